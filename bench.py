@@ -1,0 +1,271 @@
+"""Benchmark: Llama-7B per-token quantized MUL_MAT set (Q4_0, batch 1) on MI355X.
+
+BASELINE.json metric: "Q4_0 matmul GB/s + tokens/sec 7B, 1/2/4/8 MI355X vs Kotlin CPU".
+Workload (SURVEY §8d, config C4 at N=1): one step = one token of Llama-7B's matmuls,
+32 layers x {q, k, v, o: 4096x4096; gate, up: 11008x4096; down: 4096x11008}, Q4_0
+weights (llama.kotlin block layout), F32 activations, F32 outputs — 224 computeMatMul
+nodes, 3.65 GB of weights (> the 256 MiB Infinity Cache, so every step streams HBM).
+Weights are random-init N(0, 0.02^2) quantized on device; activations N(0, 1); synthetic.
+
+Multi-GPU (one process per GPU, RCCL): every weight matrix is row-sharded; rank r
+computes its rows of the 7 outputs of a layer in ONE grouped launch, then an RCCL
+all-gather (on a separate stream, overlapping the next layer) reassembles the layer's
+outputs on every rank. Total work per step is fixed -> "scaling": "strong".
+
+value = whole-job algorithmic GB/s = Σ_nodes (M·K/32·18 + 4·K + 4·M) bytes per token x
+tokens / wall time (max over ranks). tokens_per_s is reported beside it.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "llama.kotlin_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+
+HIDDEN, FFN, LAYERS = 4096, 11008, 32
+# (name, M rows, K) — LlamaConfig defaults, K/model/LlamaModel.kt:8-21; shapes :159-195, :287-304
+LAYER_MATS = [("q", HIDDEN, HIDDEN), ("k", HIDDEN, HIDDEN), ("v", HIDDEN, HIDDEN), ("o", HIDDEN, HIDDEN),
+              ("gate", FFN, HIDDEN), ("up", FFN, HIDDEN), ("down", HIDDEN, FFN)]
+Q4_0_BLOCK = 18
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def alg_bytes(M, K, N=1):
+    return M * K // 32 * Q4_0_BLOCK + 4 * K * N + 4 * M * N
+
+
+def shard(M, world, rank):
+    per = -(-M // world)
+    r0 = min(rank * per, M)
+    return r0, min(r0 + per, M)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--layers", type=int, default=LAYERS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-headline", action="store_true")
+    ap.add_argument("--cpu-sample-rows", type=int, default=6144)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import ggml_hip as G
+    G.load_library()
+    T = G.GGMLType
+
+    # ---- device-resident operands -------------------------------------------------------
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0x5EED + rank)
+    mats = []  # per layer: list of (name, M, K, r0, r1)
+    w_bytes = 0
+    for layer in range(args.layers):
+        row = []
+        for (name, M, K) in LAYER_MATS:
+            r0, r1 = shard(M, world, rank)
+            row.append((name, M, K, r0, r1))
+            w_bytes += (r1 - r0) * K // 32 * Q4_0_BLOCK
+        mats.append(row)
+    out_per_layer_local = sum(r1 - r0 for (_, _, _, r0, r1) in mats[0])
+    out_per_layer_padded = sum(-(-M // world) for (_, M, _) in LAYER_MATS)
+    ga = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+    wbuf = ga.addBuffer(w_bytes + 256)          # all Q4_0 weight shards, back to back
+    xbuf = ga.addBuffer(4 * (HIDDEN + FFN) * args.layers + 256)
+    obuf = ga.addBuffer(4 * out_per_layer_padded * args.layers + 256)
+    woff = xoff = 0
+    plans, layer_nodes = [], []
+    gathered = []
+    for layer in range(args.layers):
+        nodes = []
+        ooff = 4 * out_per_layer_padded * layer
+        for (name, M, K, r0, r1) in mats[layer]:
+            rows = r1 - r0
+            a = G.GGMLTensor(T.Q4_0, [K, rows], bufferId=wbuf, dataOffset=woff, name=f"L{layer}.{name}")
+            nb = rows * K // 32 * Q4_0_BLOCK
+            with torch.no_grad():
+                src = torch.randn(rows * K, generator=gen, device=dev, dtype=torch.float32) * 0.02
+                q = G.quantizeTensor(src, T.Q4_0)
+                ga.buffers[wbuf][woff:woff + nb].copy_(q)
+                del src, q
+            woff += (nb + 15) // 16 * 16
+            b = G.GGMLTensor(T.F32, [1, K], bufferId=xbuf, dataOffset=xoff + (0 if K == HIDDEN else 4 * HIDDEN))
+            d = G.GGMLTensor(T.F32, [1, rows], bufferId=obuf, dataOffset=ooff)
+            ooff += 4 * -(-M // world)
+            nodes.append((a, b, d))
+        xs = torch.randn(HIDDEN + FFN, generator=gen, device=dev)
+        ga.buffers[xbuf][xoff:xoff + 4 * (HIDDEN + FFN)].copy_(xs.view(torch.uint8))
+        xoff += 4 * (HIDDEN + FFN)
+        layer_nodes.append(nodes)
+        plans.append(G.MulMatPlan(ga, nodes))
+        if world > 1:
+            gathered.append(torch.empty(world * out_per_layer_padded, dtype=torch.float32, device=dev))
+    launches_per_step = sum(p.numLaunches for p in plans)
+    torch.cuda.synchronize()
+
+    compute = torch.cuda.Stream(device=dev)
+    comm = torch.cuda.Stream(device=dev)
+    obuf_f32 = ga.buffers[obuf][: 4 * out_per_layer_padded * args.layers].view(torch.float32)
+
+    def step():
+        works = []
+        with torch.cuda.stream(compute):
+            for layer, plan in enumerate(plans):
+                plan.launch(stream=compute)
+                if world > 1:
+                    ev = torch.cuda.Event()
+                    ev.record(compute)
+                    comm.wait_event(ev)
+                    with torch.cuda.stream(comm):
+                        src = obuf_f32[out_per_layer_padded * layer: out_per_layer_padded * (layer + 1)]
+                        works.append(dist.all_gather_into_tensor(gathered[layer], src, async_op=True))
+        for w in works:
+            w.wait()
+        if world > 1:
+            compute.wait_stream(comm)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(compute)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ev1.record(compute)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    token_bytes = args.layers * sum(alg_bytes(M, K) for (_, M, K) in LAYER_MATS)
+    tokens = args.steps
+    value_gbs = token_bytes * tokens / elapsed / 1e9
+    ms_per_step = elapsed * 1e3 / args.steps
+    # dominant kernel (grouped Q4_0 GEMV, one launch per layer on this rank): algorithmic bytes per
+    # launch / average launch duration from HIP events on the launch stream over the timed region
+    local_layer_bytes = sum((r1 - r0) * K // 32 * Q4_0_BLOCK + 4 * K + 4 * (r1 - r0)
+                            for (_, M, K, r0, r1) in mats[0])
+    avg_launch_s = ev_ms / 1e3 / (args.steps * launches_per_step)
+    achieved = local_layer_bytes / avg_launch_s / 1e9
+
+    result = {
+        "metric": "Q4_0 matmul GB/s + tokens/sec 7B, 1/2/4/8 MI355X vs Kotlin CPU",
+        "value": round(value_gbs, 2),
+        "unit": "GB/s",
+        "tokens_per_s": round(tokens / elapsed, 2),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "q4_0 weights x f32 activations, f32 accumulate",
+        "data": "synthetic (random-init N(0,0.02^2) weights quantized on device, N(0,1) activations)",
+        "config": {"workload": "llama7b_token_matmuls_q4_0_n1", "layers": args.layers,
+                   "matmuls_per_layer": len(LAYER_MATS), "global_batch": 1, "seq_len": 1,
+                   "bytes_per_token": token_bytes, "parallelism": f"row-shard{world}+rccl-allgather" if world > 1 else "single",
+                   "launches_per_step_per_rank": launches_per_step},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "gemv_q_n1_kernel<Q4_0> (grouped, 7 nodes per launch)",
+                     "bytes_per_launch": local_layer_bytes, "avg_launch_us": round(avg_launch_s * 1e6, 3)},
+    }
+
+    if rank == 0 and world == 1 and not args.no_headline:
+        result["headline_q4_0_4096x4096_n1"] = headline(G, ga, dev)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, token_bytes)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def headline(G, ga, dev, copies=48, reps=20):
+    """North-star shape: Q4_0 4096x4096, N=1, single computeMatMul per launch, rotating over
+    `copies` distinct weight matrices (48 x 9.4 MB = 453 MB > 256 MiB Infinity Cache)."""
+    import torch
+    T = G.GGMLType
+    M = K = 4096
+    nb = M * K // 32 * Q4_0_BLOCK
+    g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+    wb = g.addBuffer(copies * nb + 256)
+    xb = g.addBuffer(4 * K + 256)
+    db = g.addBuffer(4 * M * copies + 256)
+    src = torch.randn(M * K, device=dev) * 0.02
+    for c in range(copies):
+        g.buffers[wb][c * nb:(c + 1) * nb].copy_(G.quantizeTensor(src * (1 + 0.01 * c), T.Q4_0))
+    g.buffers[xb][: 4 * K].copy_(torch.randn(K, device=dev).view(torch.uint8))
+    nodes = [(G.GGMLTensor(T.Q4_0, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [1, K], bufferId=xb),
+              G.GGMLTensor(T.F32, [1, M], bufferId=db, dataOffset=4 * M * c)) for c in range(copies)]
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            for (a, b, d) in nodes:
+                G.computeMatMul(g, None, a, b, d, stream=s)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            for (a, b, d) in nodes:
+                G.computeMatMul(g, None, a, b, d, stream=s)
+        e1.record(s)
+    torch.cuda.synchronize()
+    per = e0.elapsed_time(e1) / 1e3 / (reps * copies)
+    gbs = alg_bytes(M, K) / per / 1e9
+    return {"launches": reps * copies, "avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(gbs, 1),
+            "frac_of_8TBps": round(gbs / HBM_PEAK_GBS, 4), "rotating_weight_copies": copies}
+
+
+def cpu_baseline(sample_rows, token_bytes):
+    """The oracle's structural restatement of computeMatMul (single thread, like the reference)
+    timed on this host over a bounded sample: the first `sample_rows` rows of each of one layer's
+    7 matrices. GB/s on the same algorithmic-bytes basis; tokens/s extrapolated by bytes."""
+    import numpy as np
+    import oracle as O
+    rng = np.random.default_rng(0)
+    total_b = 0
+    total_t = 0.0
+    for (name, M, K) in LAYER_MATS:
+        rows = min(sample_rows, M)
+        q = O.quantize(O.Q4_0, (rng.standard_normal(rows * K) * 0.02).astype(np.float32))
+        x = rng.standard_normal((K, 1)).astype(np.float32)
+        t0 = time.perf_counter()
+        O.mat_mul_q(O.Q4_0, q, rows, K, x)
+        total_t += time.perf_counter() - t0
+        total_b += alg_bytes(rows, K)
+    gbs = total_b / total_t / 1e9
+    return {"value": round(gbs, 5), "unit": "GB/s", "cores": 1, "kind": "port",
+            "tokens_per_s": round(gbs * 1e9 / token_bytes, 6),
+            "sample": f"structural C restatement of computeMatMul (oracle/lk_oracle.c), Q4_0 x F32 N=1, "
+                      f"first {sample_rows} rows of each of the 7 Llama-7B layer matrices ({total_b} algorithmic bytes, "
+                      f"{total_t:.2f} s), single thread"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+/*
+ * lk_hip.h — C-ABI of the MI355X (gfx950) backend for llama.kotlin's quantized
+ * MUL_MAT hot path.
+ *
+ * This is the drop-in boundary. Everything above it (the Kotlin/Native cinterop
+ * shim in llama.kotlin_amd/shim/, or the Python host mirror in
+ * llama.kotlin_amd/ggml_hip/) passes plain pointers and sizes; nothing below it
+ * is visible to the caller. No torch, HIP or C++ types cross this header.
+ *
+ * Reference interfaces each entry point replaces (paths relative to
+ * src/nativeMain/kotlin/ai/solace/llamakotlin/ in SolaceHarmony/llama.kotlin):
+ *
+ *   lk_mul_mat            core/GGMLComputeOps.kt:1435  fun computeMatMul(graphAllocator,
+ *                         context, a, b, dst)  — destination-tensor semantics: dst is
+ *                         pre-allocated, results land in graphAllocator.buffers[dst.bufferId]
+ *                         at dst.dataOffset, nothing is returned, inputs are not mutated.
+ *   lk_mul_mat_validate   core/GGMLComputeOps.kt:1436-1446, :1449, :1463, :1517, :1530,
+ *                         :1546, :1563 — the checks computeMatMul performs, in its order,
+ *                         without computing anything.
+ *   lk_mul_mat_device     the same operator over device-resident buffers, enqueued on a
+ *                         HIP stream (what GGMLBackend.graphCompute uses once operands
+ *                         are resident; core/GGMLBackend.kt:146).
+ *   lk_plan_*             core/GGMLBackend.kt:146 graphCompute(graph) over a graph whose
+ *                         MUL_MAT nodes are mutually independent: one launch for the set.
+ *   lk_weights_pin/evict  residency cache behind GGMLBackendBuffer.setTensor
+ *                         (core/GGMLBackend.kt:63-69) for host-authoritative ByteArrays.
+ *   lk_dequantize_device  core/GGMLComputeOps.kt:918 dequantizeTensor (Q8_0/Q4_0/Q4_1).
+ *   lk_quantize_device    core/GGMLComputeOps.kt:1040 quantizeTensor (Q8_0/Q4_0/Q4_1).
+ *
+ * Status codes map back to the exceptions the Kotlin operator throws
+ * (see INTEGRATION.md for the cinterop mapping):
+ *   LK_OK                   0  — success
+ *   LK_ERR_INVALID_ARG      1  — IllegalArgumentException (shape/type checks, require())
+ *   LK_ERR_NOT_IMPLEMENTED  2  — NotImplementedError, or "not offloaded: use the CPU path"
+ *   LK_ERR_OUT_OF_BOUNDS    3  — IndexOutOfBoundsException (accessor buffer bounds)
+ *   LK_ERR_NO_BUFFER        4  — IllegalStateException ("Tensor buffer not found")
+ *   LK_ERR_DEVICE           5  — HIP runtime failure (GGMLStatus.FAILED at backend level)
+ */
+#ifndef LK_HIP_H
+#define LK_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Type ids follow GGMLType.fromValue (core/GGMLTypes.kt:145-168). These are NOT
+ * upstream ggml/GGUF ids (Q8_0 is 6 here, 8 upstream). */
+enum lk_type {
+  LK_TYPE_F32 = 0,
+  LK_TYPE_F16 = 1,
+  LK_TYPE_Q4_0 = 2,
+  LK_TYPE_Q4_1 = 3,
+  LK_TYPE_Q5_0 = 4,
+  LK_TYPE_Q5_1 = 5,
+  LK_TYPE_Q8_0 = 6,
+  LK_TYPE_Q8_1 = 7,
+  LK_TYPE_Q2_K = 8,
+  LK_TYPE_Q3_K = 9,
+  LK_TYPE_Q4_K = 10,
+  LK_TYPE_Q5_K = 11,
+  LK_TYPE_Q6_K = 12,
+  LK_TYPE_Q8_K = 13,
+  LK_TYPE_Q1_5_K = 14,
+  LK_TYPE_I8 = 15,
+  LK_TYPE_I16 = 16,
+  LK_TYPE_I32 = 17,
+  LK_TYPE_I64 = 18,
+  LK_TYPE_BITNET_1_58 = 19 /* not in fromValue; GGMLType.BITNET_1_58 */
+};
+
+enum lk_status {
+  LK_OK = 0,
+  LK_ERR_INVALID_ARG = 1,
+  LK_ERR_NOT_IMPLEMENTED = 2,
+  LK_ERR_OUT_OF_BOUNDS = 3,
+  LK_ERR_NO_BUFFER = 4,
+  LK_ERR_DEVICE = 5
+};
+
+/* Block geometry (core/GGMLTypes.kt:84-86, :108-114): 32 weights per block.
+ *   Q4_0: f16 d | 16 B nibbles                         = 18 B
+ *   Q4_1: f16 d | f16 m | 16 B nibbles                 = 20 B
+ *   Q8_0: f16 d | 32 x int8                            = 34 B
+ * Nibble order is llama.kotlin's interleaved order: weight 2j is the low nibble
+ * of byte j, weight 2j+1 the high nibble (core/GGMLTypes.kt:647-651). */
+#define LK_QK 32
+#define LK_Q4_0_BLOCK_BYTES 18
+#define LK_Q4_1_BLOCK_BYTES 20
+#define LK_Q8_0_BLOCK_BYTES 34
+
+/* A GGMLTensor descriptor (core/GGMLTypes.kt:251-270) as the operator sees it.
+ *  - ne/nb: GGMLTensor.ne / GGMLTensor.nb (nb in bytes). Quantized tensors ignore nb,
+ *    exactly like the reference block accessors (core/GGMLTypes.kt:598-732).
+ *  - data: base address of graphAllocator.buffers[bufferId] (host ByteArray for
+ *    lk_mul_mat, device allocation for *_device). NULL = missing buffer.
+ *  - buf_bytes: size of that buffer; every access is bounds-checked against it
+ *    as the Kotlin accessors do (core/GGMLTypes.kt:360-369).
+ *  - data_offset: GGMLTensor.dataOffset. */
+typedef struct lk_tensor {
+  int32_t type;
+  int32_t reserved;
+  int64_t ne[4];
+  uint64_t nb[4];
+  void *data;
+  uint64_t buf_bytes;
+  uint64_t data_offset;
+} lk_tensor;
+
+/* ---- runtime ---------------------------------------------------------- */
+
+/* Select HIP device `device` for this thread and create the library's stream.
+ * Idempotent per device. Returns LK_OK or LK_ERR_DEVICE. */
+int lk_init(int device);
+/* Number of visible HIP devices (0 when none; never initialises a context). */
+int lk_device_count(void);
+/* Human-readable message for the last non-OK status on this thread. */
+const char *lk_last_error(void);
+/* Release the weight cache, plans and the stream. */
+void lk_shutdown(void);
+/* Library version string. */
+const char *lk_version(void);
+
+/* ---- operator ----------------------------------------------------------- */
+
+/* computeMatMul's validation only (same order, same exceptions). No device work. */
+int lk_mul_mat_validate(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst);
+
+/* computeMatMul over HOST buffers (the Kotlin drop-in): weights are copied to a
+ * device mirror (cached when pinned with lk_weights_pin), activations uploaded,
+ * the kernel runs, dst bytes are written back into dst->data before return. */
+int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst);
+
+/* computeMatMul over DEVICE buffers, enqueued on `stream` (hipStream_t; NULL =
+ * the HIP null stream of the current device). Asynchronous: returns after the
+ * launch; no allocation, no host synchronisation (graph-capturable). */
+int lk_mul_mat_device(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, void *stream);
+
+/* ---- grouped execution of independent MUL_MAT nodes ------------------------ */
+
+typedef struct lk_plan lk_plan;
+/* Validate n independent nodes (device buffers) and upload their descriptors once.
+ * Nodes with the same quant type are executed by one grouped launch each. */
+int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
+                   lk_plan **out);
+/* Enqueue every node of the plan on `stream`. */
+int lk_plan_launch(lk_plan *plan, void *stream);
+/* Number of kernel launches one lk_plan_launch issues. */
+int lk_plan_num_launches(const lk_plan *plan);
+void lk_plan_destroy(lk_plan *plan);
+
+/* ---- weight residency (host path) ------------------------------------------ */
+
+/* Copy a's bytes to a device mirror keyed by (data, data_offset, bytes, generation).
+ * A later lk_mul_mat with the same key skips the upload. */
+int lk_weights_pin(const lk_tensor *a, uint64_t generation);
+void lk_weights_evict_all(void);
+/* Bytes currently held by the weight cache. */
+uint64_t lk_weights_cached_bytes(void);
+
+/* ---- format kernels (the steps either side of the path) --------------------- */
+
+/* dequantizeTensor for Q8_0/Q4_0/Q4_1 (device buffers): writes numElements f32
+ * values (flat order) to out. Bit-exact with the reference. */
+int lk_dequantize_device(const lk_tensor *src, float *out, void *stream);
+/* quantizeTensor for a contiguous F32 source into Q8_0/Q4_0/Q4_1 block bytes
+ * (device buffers): out receives numElements/32 blocks. Bit-exact with the
+ * reference (round-half-even, Kotlin floatToHalf). */
+int lk_quantize_device(const float *src, int64_t n_elements, int32_t type, void *out,
+                       void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LK_HIP_H */

@@ -1,0 +1,558 @@
+// lk_hip.hip — host side of the C-ABI declared in include/lk_hip.h.
+//
+// Operator semantics and error behaviour mirror computeMatMul
+// (core/GGMLComputeOps.kt:1435-1565) for the node types this backend offloads:
+//   Q4_0 x F32 -> F32, Q4_1 x F32 -> F32, Q8_0 x F32 -> F32   (the hot path)
+//   F32 x F32 -> F32, F16 x F16 -> F16                         (general fallback :1530-1556)
+// Every other combination returns LK_ERR_NOT_IMPLEMENTED so the caller keeps it
+// on the CPU path (GGMLHipBackend.supportsOp == false) — this library has no CPU
+// compute of its own.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "lk_kernels.hpp"
+
+using namespace lk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int st, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return st;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess) return fail(LK_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+struct State {
+  std::mutex mu;
+  int device = -1;
+  hipStream_t stream = nullptr;
+  // weight residency cache (host path): key = (host base, offset, bytes, generation)
+  std::map<std::tuple<uintptr_t, uint64_t, uint64_t, uint64_t>, void *> weights;
+  uint64_t weight_bytes = 0;
+  // scratch for the host path
+  void *scratch[3] = {nullptr, nullptr, nullptr};
+  size_t scratch_bytes[3] = {0, 0, 0};
+};
+State &S() {
+  static State s;
+  return s;
+}
+
+int block_bytes(int32_t t) {
+  switch (t) {
+    case LK_TYPE_Q4_0: return LK_Q4_0_BLOCK_BYTES;
+    case LK_TYPE_Q4_1: return LK_Q4_1_BLOCK_BYTES;
+    case LK_TYPE_Q8_0: return LK_Q8_0_BLOCK_BYTES;
+    default: return 0;
+  }
+}
+bool is_q(int32_t t) { return block_bytes(t) != 0; }
+
+// rank / numElements (core/GGMLTypes.kt:275-300), used by getNumBlocks' bound.
+int t_rank(const lk_tensor *t) {
+  bool all_le1 = true, any_gt0 = false;
+  int last = -1;
+  for (int i = 0; i < 4; i++) {
+    if (t->ne[i] > 1) { all_le1 = false; last = i; }
+    if (t->ne[i] > 0) any_gt0 = true;
+  }
+  if (all_le1) return any_gt0 ? 1 : 0;
+  return last + 1;
+}
+int64_t t_num_elements(const lk_tensor *t) {
+  int r = t_rank(t);
+  bool all_le1 = true, any_eq0 = false;
+  for (int i = 0; i < 4; i++) {
+    if (t->ne[i] > 1) all_le1 = false;
+    if (t->ne[i] == 0) any_eq0 = true;
+  }
+  if (r == 0 && all_le1) return 1;
+  if (r == 0 && any_eq0) return 0;
+  int64_t c = 1;
+  for (int i = 0; i < std::max(r, 1); i++) {
+    if (t->ne[i] == 0 && r > 1) return 0;
+    if (t->ne[i] > 0) c *= t->ne[i];
+  }
+  return c;
+}
+
+// Byte footprint [lo, hi) of a 2-D strided element tensor read at (i0<n0, i1<n1).
+void span2(const lk_tensor *t, int64_t n0, int64_t n1, uint64_t width, uint64_t *lo, uint64_t *hi) {
+  *lo = t->data_offset;
+  *hi = t->data_offset + (uint64_t)(n0 - 1) * t->nb[0] + (uint64_t)(n1 - 1) * t->nb[1] + width;
+}
+
+enum class Path { kQuantF32, kF32, kF16 };
+
+struct Checked {
+  Path path;
+  int64_t M, N, K;
+  uint64_t a_lo, a_hi, b_lo, b_hi, d_lo, d_hi; // byte footprints (absolute in the buffers)
+  bool empty;                                   // M*N == 0: nothing is read or written
+};
+
+// computeMatMul's checks (core/GGMLComputeOps.kt:1436-1564) for what this backend offloads.
+// Errors the Kotlin loop would raise on its first faulting access are reported up front
+// (dst may then hold a partial result on the CPU path; here dst is left untouched).
+int check(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, Checked *c) {
+  if (!a || !b || !dst) return fail(LK_ERR_INVALID_ARG, "null tensor descriptor");
+  const int64_t M = a->ne[1], K_a = a->ne[0], N = b->ne[0], K_b = b->ne[1];
+  if (K_a != K_b) /* :1440 */
+    return fail(LK_ERR_INVALID_ARG, "Dim mismatch K: a.ne[0](%lld) != b.ne[1](%lld)", (long long)K_a, (long long)K_b);
+  const int64_t K = K_a;
+  if (dst->ne[0] != N || dst->ne[1] != M) /* :1444-1446 */
+    return fail(LK_ERR_INVALID_ARG,
+                "Result tensor dimensions must match expected output size: expected [%lld, %lld], got [%lld, %lld]",
+                (long long)N, (long long)M, (long long)dst->ne[0], (long long)dst->ne[1]);
+  c->M = M; c->N = N; c->K = K;
+  c->empty = (M <= 0 || N <= 0);
+  if (is_q(a->type) && b->type == LK_TYPE_F32) {
+    if (dst->type != LK_TYPE_F32) /* :1449, :1463, :1517 */
+      return fail(LK_ERR_INVALID_ARG, "Result tensor type must be F32 for quantized x F32 matmul");
+    c->path = Path::kQuantF32;
+  } else if (b->type == LK_TYPE_F32 && (a->type == LK_TYPE_Q2_K || a->type == LK_TYPE_Q4_K || a->type == LK_TYPE_Q8_K)) {
+    return fail(LK_ERR_NOT_IMPLEMENTED, "K-quant x F32 is not offloaded (CPU path)");
+  } else {
+    if (dst->type != a->type) /* :1530 */
+      return fail(LK_ERR_INVALID_ARG, "Result tensor type must match first input type for general matmul");
+    if (a->type == LK_TYPE_F32 && b->type == LK_TYPE_F32) c->path = Path::kF32;
+    else if (a->type == LK_TYPE_F16 && b->type == LK_TYPE_F16) c->path = Path::kF16;
+    else return fail(LK_ERR_NOT_IMPLEMENTED, "type combination (%d x %d) is not offloaded (CPU path)", a->type, b->type);
+  }
+  if (c->empty) return LK_OK;
+  if (!dst->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found (dst)");
+  if (K > 0) {
+    if (!a->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found (a)");
+    if (!b->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found (b)");
+  }
+  const uint64_t ew = (c->path == Path::kF16) ? 2 : 4;
+  // device loads need natural alignment of element tensors
+  auto misaligned = [&](const lk_tensor *t) {
+    return (((uintptr_t)t->data + t->data_offset) % ew) || (t->nb[0] % ew) || (t->nb[1] % ew);
+  };
+  if (K > 0) {
+    if (c->path == Path::kQuantF32) {
+      // getNumBlocks bound (core/GGMLTypes.kt:598-602): last block touched is (M*K-1)/32.
+      const int64_t last_blk = (M * K - 1) / 32;
+      const int64_t nblk = t_num_elements(a) / 32;
+      if (last_blk >= nblk)
+        return fail(LK_ERR_INVALID_ARG, "blockIndex %lld out of bounds for %lld blocks", (long long)last_blk, (long long)nblk);
+      c->a_lo = a->data_offset;
+      c->a_hi = a->data_offset + (uint64_t)(last_blk + 1) * block_bytes(a->type);
+      if (c->a_hi > a->buf_bytes)
+        return fail(LK_ERR_OUT_OF_BOUNDS, "quant block read ends at %llu, out of buffer bounds %llu",
+                    (unsigned long long)c->a_hi, (unsigned long long)a->buf_bytes);
+    } else {
+      span2(a, K, M, ew, &c->a_lo, &c->a_hi);
+      if (c->a_hi > a->buf_bytes)
+        return fail(LK_ERR_OUT_OF_BOUNDS, "Calculated offset %llu is out of bounds for buffer size %llu",
+                    (unsigned long long)(c->a_hi - ew), (unsigned long long)a->buf_bytes);
+      if (misaligned(a)) return fail(LK_ERR_NOT_IMPLEMENTED, "unaligned element strides for a (CPU path)");
+    }
+    span2(b, N, K, ew, &c->b_lo, &c->b_hi);
+    if (c->b_hi > b->buf_bytes)
+      return fail(LK_ERR_OUT_OF_BOUNDS, "Calculated offset %llu is out of bounds for buffer size %llu",
+                  (unsigned long long)(c->b_hi - ew), (unsigned long long)b->buf_bytes);
+    if (misaligned(b)) return fail(LK_ERR_NOT_IMPLEMENTED, "unaligned element strides for b (CPU path)");
+  } else {
+    c->a_lo = c->a_hi = a->data_offset;
+    c->b_lo = c->b_hi = b->data_offset;
+  }
+  span2(dst, N, M, ew, &c->d_lo, &c->d_hi);
+  if (c->d_hi > dst->buf_bytes)
+    return fail(LK_ERR_OUT_OF_BOUNDS, "Calculated offset %llu is out of bounds for buffer size %llu",
+                (unsigned long long)(c->d_hi - ew), (unsigned long long)dst->buf_bytes);
+  if (misaligned(dst)) return fail(LK_ERR_NOT_IMPLEMENTED, "unaligned element strides for dst (CPU path)");
+  return LK_OK;
+}
+
+// Device entry points run on the caller's stream; NULL is the HIP null (default) stream,
+// so they order with whatever the caller last enqueued there.
+hipStream_t pick_stream(void *s) { return (hipStream_t)s; }
+
+// Fast grouped GEMV eligibility: batch 1, K % 64 == 0, 4-byte aligned A, 16-byte
+// aligned contiguous x, F32 dst with unit column stride irrelevant (N == 1).
+bool gemv_eligible(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const Checked &c) {
+  if (c.path != Path::kQuantF32 || c.N != 1 || c.K <= 0 || (c.K % 64) != 0) return false;
+  if (c.M > (int64_t)INT32_MAX || c.K > (int64_t)INT32_MAX) return false;
+  if (((uintptr_t)a->data + a->data_offset) % 4) return false;
+  if (((uintptr_t)b->data + b->data_offset) % 16) return false;
+  if (c.K > 1 && b->nb[1] != 4) return false; // x(k) = B(0,k) contiguous
+  if (dst->nb[1] % 4) return false;
+  return true;
+}
+
+constexpr int kRowsQ4 = 4;
+constexpr int kRowsQ8 = 2;
+int rows_per_wave(int32_t qt) { return qt == LK_TYPE_Q8_0 ? kRowsQ8 : kRowsQ4; }
+
+GemvDesc make_desc(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const Checked &c) {
+  GemvDesc d{};
+  d.a = (const uint8_t *)a->data + a->data_offset;
+  d.x = (const float *)((const uint8_t *)b->data + b->data_offset);
+  d.dst = (float *)((uint8_t *)dst->data + dst->data_offset);
+  d.dst_row_stride = (int64_t)(dst->nb[1] / 4);
+  d.M = (int32_t)c.M;
+  d.K = (int32_t)c.K;
+  return d;
+}
+
+int launch_gemv_group(int32_t qt, const GemvDesc &single, const GemvDesc *ddescs, const uint16_t *dmap, int ntiles,
+                      hipStream_t st) {
+  if (ntiles <= 0) return LK_OK;
+  dim3 grid(ntiles), block(256);
+  switch (qt) {
+    case LK_TYPE_Q4_0: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q4_0, kRowsQ4>), grid, block, 0, st, single, ddescs, dmap); break;
+    case LK_TYPE_Q4_1: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q4_1, kRowsQ4>), grid, block, 0, st, single, ddescs, dmap); break;
+    case LK_TYPE_Q8_0: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q8_0, kRowsQ8>), grid, block, 0, st, single, ddescs, dmap); break;
+    default: return fail(LK_ERR_NOT_IMPLEMENTED, "gemv: type %d", qt);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  GenericArgs g{};
+  g.a = (const uint8_t *)a->data + a->data_offset;
+  g.b = (const uint8_t *)b->data + b->data_offset;
+  g.dst = (uint8_t *)dst->data + dst->data_offset;
+  g.M = c.M; g.N = c.N; g.K = c.K;
+  g.a_nb0 = a->nb[0]; g.a_nb1 = a->nb[1];
+  g.b_nb0 = b->nb[0]; g.b_nb1 = b->nb[1];
+  g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
+  const int64_t waves = c.M * c.N;
+  const int64_t blocks = (waves + 3) / 4;
+  if (blocks > (int64_t)INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "output too large for the generic kernel");
+  dim3 grid((unsigned)blocks), block(256);
+  int32_t t = (c.path == Path::kQuantF32) ? a->type : (c.path == Path::kF32 ? LK_TYPE_F32 : LK_TYPE_F16);
+  switch (t) {
+    case LK_TYPE_Q4_0: hipLaunchKernelGGL(mul_mat_generic_kernel<LK_TYPE_Q4_0>, grid, block, 0, st, g); break;
+    case LK_TYPE_Q4_1: hipLaunchKernelGGL(mul_mat_generic_kernel<LK_TYPE_Q4_1>, grid, block, 0, st, g); break;
+    case LK_TYPE_Q8_0: hipLaunchKernelGGL(mul_mat_generic_kernel<LK_TYPE_Q8_0>, grid, block, 0, st, g); break;
+    case LK_TYPE_F32: hipLaunchKernelGGL(mul_mat_generic_kernel<LK_TYPE_F32>, grid, block, 0, st, g); break;
+    case LK_TYPE_F16: hipLaunchKernelGGL(mul_mat_generic_kernel<LK_TYPE_F16>, grid, block, 0, st, g); break;
+    default: return fail(LK_ERR_NOT_IMPLEMENTED, "generic: type %d", t);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+// Single eligible GEMV: the descriptor travels in the kernel arguments (no
+// allocation, no host sync: stream-ordered and graph-capturable).
+int run_single_gemv(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  const int rows_per_tile = kGemvWaves * rows_per_wave(a->type);
+  const int64_t ntiles = (c.M + rows_per_tile - 1) / rows_per_tile;
+  if (ntiles > INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "too many rows");
+  GemvDesc d = make_desc(a, b, dst, c);
+  d.tile_begin = 0;
+  return launch_gemv_group(a->type, d, nullptr, nullptr, (int)ntiles, st);
+}
+
+int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  if (c.empty) return LK_OK;
+  if (c.K == 0) { // every dot product is the empty sum: dst := 0 (F32 or F16 +0.0)
+    if (dst->nb[0] == (c.path == Path::kF16 ? 2u : 4u) && dst->nb[1] == dst->nb[0] * (uint64_t)c.N) {
+      HIP_TRY(hipMemsetAsync((uint8_t *)dst->data + dst->data_offset, 0, (size_t)(c.d_hi - c.d_lo), st));
+      return LK_OK;
+    }
+    return launch_generic(a, b, dst, c, st);
+  }
+  if (gemv_eligible(a, b, dst, c)) return run_single_gemv(a, b, dst, c, st);
+  return launch_generic(a, b, dst, c, st);
+}
+
+int ensure_scratch(int idx, size_t bytes) {
+  State &s = S();
+  if (s.scratch_bytes[idx] >= bytes) return LK_OK;
+  if (s.scratch[idx]) HIP_TRY(hipFree(s.scratch[idx]));
+  s.scratch[idx] = nullptr;
+  s.scratch_bytes[idx] = 0;
+  size_t want = std::max<size_t>(bytes, 1 << 20);
+  HIP_TRY(hipMalloc(&s.scratch[idx], want));
+  s.scratch_bytes[idx] = want;
+  return LK_OK;
+}
+
+// Lazily create the library stream on the caller's CURRENT device (a rank that
+// selected device r keeps device r).
+int ensure_init() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (S().stream && S().device == dev) return LK_OK;
+  return lk_init(dev);
+}
+
+}  // namespace
+
+// ============================================================================
+// C-ABI
+// ============================================================================
+
+extern "C" {
+
+const char *lk_version(void) { return "lk_hip 0.1 (gfx950)"; }
+
+const char *lk_last_error(void) { return g_err.c_str(); }
+
+int lk_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int lk_init(int device) {
+  State &s = S();
+  std::lock_guard<std::mutex> lk(s.mu);
+  if (s.stream && s.device == device) return LK_OK;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(LK_ERR_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(LK_ERR_INVALID_ARG, "device %d out of range (%d devices)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  if (s.stream) HIP_TRY(hipStreamDestroy(s.stream));
+  HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  s.device = device;
+  return LK_OK;
+}
+
+void lk_weights_evict_all(void) {
+  State &s = S();
+  for (auto &kv : s.weights) (void)hipFree(kv.second);
+  s.weights.clear();
+  s.weight_bytes = 0;
+}
+
+uint64_t lk_weights_cached_bytes(void) { return S().weight_bytes; }
+
+void lk_shutdown(void) {
+  State &s = S();
+  if (!s.stream) return;
+  (void)hipStreamSynchronize(s.stream);
+  lk_weights_evict_all();
+  for (int i = 0; i < 3; i++) {
+    if (s.scratch[i]) (void)hipFree(s.scratch[i]);
+    s.scratch[i] = nullptr;
+    s.scratch_bytes[i] = 0;
+  }
+  (void)hipStreamDestroy(s.stream);
+  s.stream = nullptr;
+  s.device = -1;
+}
+
+int lk_mul_mat_validate(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst) {
+  Checked c;
+  return check(a, b, dst, &c);
+}
+
+int lk_mul_mat_device(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, void *stream) {
+  Checked c;
+  int rc = check(a, b, dst, &c);
+  if (rc) return rc;
+  return mul_mat_device_checked(a, b, dst, c, pick_stream(stream));
+}
+
+int lk_weights_pin(const lk_tensor *a, uint64_t generation) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  if (!a || !a->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
+  uint64_t bytes;
+  if (is_q(a->type)) bytes = (uint64_t)(t_num_elements(a) / 32) * block_bytes(a->type);
+  else bytes = (uint64_t)t_num_elements(a) * (a->type == LK_TYPE_F16 ? 2 : 4);
+  if (a->data_offset + bytes > a->buf_bytes) return fail(LK_ERR_OUT_OF_BOUNDS, "pin: tensor exceeds its buffer");
+  State &s = S();
+  auto key = std::make_tuple((uintptr_t)a->data, a->data_offset, bytes, generation);
+  if (s.weights.count(key)) return LK_OK;
+  void *dev = nullptr;
+  HIP_TRY(hipMalloc(&dev, std::max<uint64_t>(bytes, 4)));
+  HIP_TRY(hipMemcpy(dev, (const uint8_t *)a->data + a->data_offset, bytes, hipMemcpyHostToDevice));
+  s.weights[key] = dev;
+  s.weight_bytes += bytes;
+  return LK_OK;
+}
+
+// Host-buffer operator: the Kotlin drop-in. ByteArrays stay authoritative; A comes
+// from the residency cache when pinned (any generation matching the host range),
+// otherwise it is staged per call.
+int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
+  Checked c;
+  int rc = check(a, b, dst, &c);
+  if (rc) return rc;
+  if (c.empty) return LK_OK;
+  rc = ensure_init();
+  if (rc) return rc;
+  State &s = S();
+  hipStream_t st = s.stream;
+  const uint64_t a_bytes = c.a_hi - c.a_lo, b_bytes = c.b_hi - c.b_lo, d_bytes = c.d_hi - c.d_lo;
+  // A: cached mirror or staged copy
+  const void *a_dev = nullptr;
+  for (auto &kv : s.weights) {
+    auto [base, off, bytes, gen] = kv.first;
+    (void)gen;
+    if (base == (uintptr_t)a->data && off <= c.a_lo && c.a_hi <= off + bytes) {
+      a_dev = (const uint8_t *)kv.second + (c.a_lo - off);
+      break;
+    }
+  }
+  if (!a_dev && a_bytes) {
+    if ((rc = ensure_scratch(0, a_bytes))) return rc;
+    HIP_TRY(hipMemcpyAsync(s.scratch[0], (const uint8_t *)a->data + c.a_lo, a_bytes, hipMemcpyHostToDevice, st));
+    a_dev = s.scratch[0];
+  }
+  if ((rc = ensure_scratch(1, std::max<uint64_t>(b_bytes, 16)))) return rc;
+  if ((rc = ensure_scratch(2, d_bytes))) return rc;
+  if (b_bytes) HIP_TRY(hipMemcpyAsync(s.scratch[1], (const uint8_t *)b->data + c.b_lo, b_bytes, hipMemcpyHostToDevice, st));
+  // strided dst: preserve the bytes between written elements
+  HIP_TRY(hipMemcpyAsync(s.scratch[2], (const uint8_t *)dst->data + c.d_lo, d_bytes, hipMemcpyHostToDevice, st));
+  lk_tensor da = *a, db = *b, dd = *dst;
+  da.data = const_cast<void *>(a_dev); da.data_offset = 0; da.buf_bytes = a_bytes;
+  db.data = s.scratch[1]; db.data_offset = 0; db.buf_bytes = b_bytes;
+  dd.data = s.scratch[2]; dd.data_offset = 0; dd.buf_bytes = d_bytes;
+  Checked cd = c;
+  cd.a_lo = 0; cd.a_hi = a_bytes; cd.b_lo = 0; cd.b_hi = b_bytes; cd.d_lo = 0; cd.d_hi = d_bytes;
+  rc = mul_mat_device_checked(&da, &db, &dd, cd, st);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync((uint8_t *)dst->data + c.d_lo, s.scratch[2], d_bytes, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return LK_OK;
+}
+
+// ---- plans: independent MUL_MAT nodes, one grouped launch per quant type ----------
+
+struct lk_plan {
+  struct Group { int32_t qt; int ntiles; void *dev; const GemvDesc *descs; const uint16_t *map; };
+  std::vector<Group> groups;
+  struct Single { lk_tensor a, b, d; Checked c; };
+  std::vector<Single> singles;
+};
+
+int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n, lk_plan **out) {
+  if (!out || n < 0) return fail(LK_ERR_INVALID_ARG, "bad plan arguments");
+  int rc = ensure_init();
+  if (rc) return rc;
+  auto plan = new lk_plan();
+  std::map<int32_t, std::vector<GemvDesc>> by_type;
+  std::map<int32_t, int64_t> tiles;
+  for (int i = 0; i < n; i++) {
+    Checked c;
+    rc = check(&a[i], &b[i], &dst[i], &c);
+    if (rc) { delete plan; return rc; }
+    if (c.empty) continue;
+    if (gemv_eligible(&a[i], &b[i], &dst[i], c)) {
+      GemvDesc d = make_desc(&a[i], &b[i], &dst[i], c);
+      const int rpt = kGemvWaves * rows_per_wave(a[i].type);
+      d.tile_begin = (int32_t)tiles[a[i].type];
+      tiles[a[i].type] += (c.M + rpt - 1) / rpt;
+      by_type[a[i].type].push_back(d);
+    } else {
+      plan->singles.push_back({a[i], b[i], dst[i], c});
+    }
+  }
+  for (auto &kv : by_type) {
+    const int32_t qt = kv.first;
+    auto &descs = kv.second;
+    const int64_t nt = tiles[qt];
+    if (nt > INT32_MAX || descs.size() > 65535) { delete plan; return fail(LK_ERR_NOT_IMPLEMENTED, "plan too large"); }
+    std::vector<uint16_t> map((size_t)nt);
+    for (size_t di = 0; di < descs.size(); di++) {
+      int64_t end = (di + 1 < descs.size()) ? descs[di + 1].tile_begin : nt;
+      for (int64_t t = descs[di].tile_begin; t < end; t++) map[(size_t)t] = (uint16_t)di;
+    }
+    const size_t db = descs.size() * sizeof(GemvDesc), mb = map.size() * sizeof(uint16_t);
+    void *dev = nullptr;
+    if (hipMalloc(&dev, db + mb) != hipSuccess) { delete plan; return fail(LK_ERR_DEVICE, "plan alloc"); }
+    if (hipMemcpy(dev, descs.data(), db, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy((uint8_t *)dev + db, map.data(), mb, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(dev);
+      delete plan;
+      return fail(LK_ERR_DEVICE, "plan upload");
+    }
+    plan->groups.push_back({qt, (int)nt, dev, (const GemvDesc *)dev, (const uint16_t *)((uint8_t *)dev + db)});
+  }
+  *out = plan;
+  return LK_OK;
+}
+
+int lk_plan_launch(lk_plan *plan, void *stream) {
+  if (!plan) return fail(LK_ERR_INVALID_ARG, "null plan");
+  hipStream_t st = pick_stream(stream);
+  for (auto &g : plan->groups) {
+    int rc = launch_gemv_group(g.qt, GemvDesc{}, g.descs, g.map, g.ntiles, st);
+    if (rc) return rc;
+  }
+  for (auto &s : plan->singles) {
+    int rc = mul_mat_device_checked(&s.a, &s.b, &s.d, s.c, st);
+    if (rc) return rc;
+  }
+  return LK_OK;
+}
+
+int lk_plan_num_launches(const lk_plan *plan) {
+  return plan ? (int)(plan->groups.size() + plan->singles.size()) : 0;
+}
+
+void lk_plan_destroy(lk_plan *plan) {
+  if (!plan) return;
+  for (auto &g : plan->groups) (void)hipFree(g.dev);
+  delete plan;
+}
+
+// ---- format kernels ----------------------------------------------------------------
+
+int lk_dequantize_device(const lk_tensor *src, float *out, void *stream) {
+  if (!src) return fail(LK_ERR_INVALID_ARG, "null tensor");
+  if (!is_q(src->type)) return fail(LK_ERR_NOT_IMPLEMENTED, "dequantize: type %d not offloaded", src->type);
+  if (!src->data || !out) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
+  const int64_t nblk = t_num_elements(src) / 32;
+  if (src->data_offset + (uint64_t)nblk * block_bytes(src->type) > src->buf_bytes)
+    return fail(LK_ERR_OUT_OF_BOUNDS, "dequantize: blocks exceed buffer");
+  if (nblk == 0) return LK_OK;
+  hipStream_t st = pick_stream(stream);
+  const uint8_t *p = (const uint8_t *)src->data + src->data_offset;
+  dim3 grid((unsigned)((nblk + 255) / 256)), block(256);
+  switch (src->type) {
+    case LK_TYPE_Q4_0: hipLaunchKernelGGL(dequantize_kernel<LK_TYPE_Q4_0>, grid, block, 0, st, p, out, nblk); break;
+    case LK_TYPE_Q4_1: hipLaunchKernelGGL(dequantize_kernel<LK_TYPE_Q4_1>, grid, block, 0, st, p, out, nblk); break;
+    default: hipLaunchKernelGGL(dequantize_kernel<LK_TYPE_Q8_0>, grid, block, 0, st, p, out, nblk); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+int lk_quantize_device(const float *src, int64_t n, int32_t type, void *out, void *stream) {
+  if (!is_q(type)) return fail(LK_ERR_NOT_IMPLEMENTED, "quantize: type %d not offloaded", type);
+  if (n % 32 != 0) return fail(LK_ERR_INVALID_ARG, "numElements %lld not div by 32", (long long)n); /* :1062, :1074, :1089 */
+  if (n == 0) return LK_OK;
+  if (!src || !out) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
+  hipStream_t st = pick_stream(stream);
+  const int64_t nblk = n / 32;
+  dim3 grid((unsigned)((nblk + 255) / 256)), block(256);
+  switch (type) {
+    case LK_TYPE_Q4_0: hipLaunchKernelGGL(quantize_kernel<LK_TYPE_Q4_0>, grid, block, 0, st, src, (uint8_t *)out, nblk); break;
+    case LK_TYPE_Q4_1: hipLaunchKernelGGL(quantize_kernel<LK_TYPE_Q4_1>, grid, block, 0, st, src, (uint8_t *)out, nblk); break;
+    default: hipLaunchKernelGGL(quantize_kernel<LK_TYPE_Q8_0>, grid, block, 0, st, src, (uint8_t *)out, nblk); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,38 @@
+"""ggml_hip — MI355X (gfx950) backend for llama.kotlin's quantized MUL_MAT path.
+
+Host-side mirror of the reference's operator/plugin API for this path, over the
+C-ABI in include/lk_hip.h (liblk_hip.so, hand-written HIP kernels):
+
+  computeMatMul(graphAllocator, context, a, b, dst)  core/GGMLComputeOps.kt:1435
+  GGMLTensor / GGMLGraphAllocator / GGMLType          core/GGMLTypes.kt, core/GGMLAlloc.kt
+  GGMLHipBackend (GGMLBackend)                        core/GGMLBackend.kt:90-157
+  dequantizeTensor / quantizeTensor (device)          core/GGMLComputeOps.kt:918 / :1040
+  RowShardedMulMat (rows over GPUs + RCCL gather)     new: the reference is single-device
+
+There is no CPU compute path in this package: a missing liblk_hip.so raises.
+"""
+from . import _lib
+from ._lib import (HipDeviceError, IllegalArgumentException, IllegalStateException, IndexOutOfBoundsException,
+                   NotOffloadedError)
+from .backend import GGMLBackendRegistry, GGMLHipBackend, GGMLStatus
+from .ops import (MulMatPlan, computeMatMul, dequantizeTensor, quantizeTensor, to_lk, validateMatMul, weightsEvictAll,
+                  weightsPin)
+from .sharded import RowShardedMulMat, row_slice, shard_rows
+from .tensor import (GGMLCGraph, GGMLContext, GGMLGraphAllocator, GGMLOp, GGMLTensor, GGMLType,
+                     calculateContiguousStrides, calculateTensorByteSize)
+
+__all__ = [
+    "GGMLType", "GGMLTensor", "GGMLGraphAllocator", "GGMLContext", "GGMLCGraph", "GGMLOp",
+    "calculateContiguousStrides", "calculateTensorByteSize",
+    "computeMatMul", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+    "weightsEvictAll", "to_lk",
+    "GGMLHipBackend", "GGMLStatus", "GGMLBackendRegistry",
+    "RowShardedMulMat", "row_slice", "shard_rows",
+    "IllegalArgumentException", "IndexOutOfBoundsException", "IllegalStateException", "NotOffloadedError",
+    "HipDeviceError",
+]
+
+
+def load_library():
+    """Load liblk_hip.so now (raises ImportError if it was not built)."""
+    return _lib.load()

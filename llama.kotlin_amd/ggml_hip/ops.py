@@ -1,0 +1,151 @@
+"""The MUL_MAT operator over the HIP C-ABI, mirroring the reference's signatures.
+
+  computeMatMul(graphAllocator, context, a, b, dst)
+      core/GGMLComputeOps.kt:1435 — destination-tensor semantics: dst is pre-allocated,
+      results land in graphAllocator.buffers[dst.bufferId] at dst.dataOffset, nothing is
+      returned, inputs are never mutated. Exceptions as the Kotlin operator throws them
+      (IllegalArgumentException / IndexOutOfBoundsException / IllegalStateException /
+      NotImplementedError); see _lib.raise_for_status.
+  dequantizeTensor / quantizeTensor
+      core/GGMLComputeOps.kt:918 / :1040, on device (the format steps either side of the
+      path).
+
+Device buffers go through lk_mul_mat_device on the current torch stream (asynchronous,
+no host sync); host buffers through lk_mul_mat (the Kotlin ByteArray drop-in).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .tensor import GGMLCGraph, GGMLContext, GGMLGraphAllocator, GGMLTensor, GGMLType, calculateTensorByteSize
+
+
+def _is_host(ga: GGMLGraphAllocator, t: GGMLTensor) -> bool:
+    if t.bufferId < 0 or t.bufferId >= len(ga.buffers):
+        return ga.device == "host"
+    return isinstance(ga.buffers[t.bufferId], np.ndarray)
+
+
+def to_lk(ga: GGMLGraphAllocator, t: GGMLTensor) -> _lib.LkTensor:
+    """GGMLTensor -> lk_tensor (buffer base, size and dataOffset; NULL for a missing buffer)."""
+    lt = _lib.LkTensor()
+    lt.type = int(t.type)
+    for i in range(4):
+        lt.ne[i] = int(t.ne[i])
+        lt.nb[i] = int(t.nb[i])
+    if 0 <= t.bufferId < len(ga.buffers) and ga.buffers[t.bufferId] is not None:
+        lt.data = ga.dataPtr(t.bufferId)
+        lt.buf_bytes = ga.bufferSize(t.bufferId)
+    else:
+        lt.data = None
+        lt.buf_bytes = 0
+    lt.data_offset = int(t.dataOffset)
+    return lt
+
+
+def _stream_handle(stream=None) -> int | None:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def computeMatMul(graphAllocator: GGMLGraphAllocator, context: GGMLContext | None, a: GGMLTensor, b: GGMLTensor,
+                  dst: GGMLTensor, stream=None) -> None:
+    """core/GGMLComputeOps.kt:1435 on the MI355X. ``context`` is unused, as in the reference."""
+    L = _lib.load()
+    la, lb, ld = to_lk(graphAllocator, a), to_lk(graphAllocator, b), to_lk(graphAllocator, dst)
+    host = [_is_host(graphAllocator, t) for t in (a, b, dst)]
+    if all(host):
+        st = L.lk_mul_mat(ctypes.byref(la), ctypes.byref(lb), ctypes.byref(ld))
+    elif not any(host):
+        st = L.lk_mul_mat_device(ctypes.byref(la), ctypes.byref(lb), ctypes.byref(ld), _stream_handle(stream))
+    else:
+        raise _lib.IllegalArgumentException("operands must all be host or all be device buffers")
+    _lib.check(st)
+
+
+def validateMatMul(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, b: GGMLTensor, dst: GGMLTensor) -> int:
+    """computeMatMul's checks only; returns the lk_status code (0 = would run)."""
+    L = _lib.load()
+    return L.lk_mul_mat_validate(ctypes.byref(to_lk(graphAllocator, a)), ctypes.byref(to_lk(graphAllocator, b)),
+                                 ctypes.byref(to_lk(graphAllocator, dst)))
+
+
+class MulMatPlan:
+    """Independent MUL_MAT nodes prepared once and launched together
+    (GGMLBackend.graphCompute over such a graph, core/GGMLBackend.kt:146): nodes of
+    one quant type share a single grouped kernel launch."""
+
+    def __init__(self, ga: GGMLGraphAllocator, nodes):
+        L = _lib.load()
+        n = len(nodes)
+        A = (_lib.LkTensor * max(n, 1))()
+        B = (_lib.LkTensor * max(n, 1))()
+        D = (_lib.LkTensor * max(n, 1))()
+        for i, (a, b, d) in enumerate(nodes):
+            A[i], B[i], D[i] = to_lk(ga, a), to_lk(ga, b), to_lk(ga, d)
+        self._handle = ctypes.c_void_p()
+        _lib.check(L.lk_plan_create(A, B, D, n, ctypes.byref(self._handle)))
+        self._keep = (A, B, D)
+
+    @property
+    def numLaunches(self) -> int:
+        return _lib.load().lk_plan_num_launches(self._handle)
+
+    def launch(self, stream=None):
+        _lib.check(_lib.load().lk_plan_launch(self._handle, _stream_handle(stream)))
+
+    def close(self):
+        if self._handle:
+            _lib.load().lk_plan_destroy(self._handle)
+            self._handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def dequantizeTensor(graphAllocator: GGMLGraphAllocator, tensor: GGMLTensor, stream=None):
+    """core/GGMLComputeOps.kt:918 for Q8_0/Q4_0/Q4_1 on device: returns a float32 torch tensor
+    of numElements values (bit-exact with the reference)."""
+    import torch
+    L = _lib.load()
+    n = tensor.getNumBlocks() * 32
+    out = torch.empty(n, dtype=torch.float32, device=graphAllocator.buffers[tensor.bufferId].device)
+    _lib.check(L.lk_dequantize_device(ctypes.byref(to_lk(graphAllocator, tensor)), ctypes.c_void_p(out.data_ptr()),
+                                      _stream_handle(stream)))
+    return out
+
+
+def quantizeTensor(src, targetType: GGMLType, stream=None):
+    """core/GGMLComputeOps.kt:1040 for a contiguous device F32 torch tensor -> uint8 block bytes
+    (bit-exact: round-half-even, Kotlin floatToHalf)."""
+    import torch
+    L = _lib.load()
+    src = src.contiguous().view(-1)
+    if src.dtype != torch.float32:
+        raise _lib.IllegalArgumentException(f"quantizeTensor expects F32 input, got {src.dtype}")
+    n = src.numel()
+    bs = GGMLType(targetType).byteSize
+    out = torch.empty((n // 32) * bs if n % 32 == 0 else 0, dtype=torch.uint8, device=src.device)
+    _lib.check(L.lk_quantize_device(ctypes.c_void_p(src.data_ptr()), n, int(targetType),
+                                    ctypes.c_void_p(out.data_ptr() if out.numel() else 0), _stream_handle(stream)))
+    return out
+
+
+def weightsPin(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, generation: int = 0):
+    """Host path: keep a device mirror of a's bytes (GGMLBackendBuffer.setTensor residency)."""
+    _lib.check(_lib.load().lk_weights_pin(ctypes.byref(to_lk(graphAllocator, a)), generation))
+
+
+def weightsEvictAll():
+    _lib.load().lk_weights_evict_all()
+
+
+__all__ = ["computeMatMul", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+           "weightsEvictAll", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]

@@ -1,0 +1,109 @@
+"""Row-sharded MUL_MAT across the GPUs of one node (one process per GPU, RCCL over xGMI).
+
+The reference has no multi-device code; this is the north star's design:
+the dot products dst(j,i) are independent per output row i, so rank r owns rows
+[r0, r1) of the weight matrix A — one contiguous byte range, because a row is
+K/32 blocks — computes the matching contiguous [N x (r1-r0)] slice of dst, and one
+all-gather (torch.distributed over the "nccl" backend = RCCL) reassembles the full
+dst on every rank (the next layer needs every output row). B is replicated.
+
+Shards are balanced with equal sizes (ceil(M/P) rows; the last rank may own fewer
+real rows and the gather buffer is padded) so the collective is a single
+all_gather_into_tensor on one contiguous buffer.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+from .tensor import GGMLGraphAllocator, GGMLTensor, GGMLType
+
+
+def shard_rows(M: int, world: int, rank: int) -> tuple[int, int]:
+    """Rows [r0, r1) owned by `rank` under the equal-size split (ceil(M/world) per rank)."""
+    per = -(-M // world) if world > 0 else M
+    r0 = min(rank * per, M)
+    return r0, min(r0 + per, M)
+
+
+def row_bytes(t: GGMLTensor) -> int:
+    """Bytes of one row of A (ne[0] = K elements): K/32 blocks for block types."""
+    K = t.ne[0]
+    if t.type.isBlockQuantized:
+        if K % 32:
+            raise ValueError("row sharding needs K % 32 == 0 so rows are whole blocks")
+        return K // 32 * t.type.byteSize
+    return t.nb[1]
+
+
+def row_slice(t: GGMLTensor, r0: int, r1: int, name: str = "") -> GGMLTensor:
+    """A view of rows [r0, r1) of a 2-D tensor (A: ne=[K,M]; dst: ne=[N,M])."""
+    s = GGMLTensor(t.type, [t.ne[0], r1 - r0, 1, 1], nb=list(t.nb), name=name or t.name,
+                   bufferId=t.bufferId, dataOffset=t.dataOffset + r0 * row_bytes(t))
+    return s
+
+
+@dataclass
+class ShardSpec:
+    world: int
+    rank: int
+    M: int
+
+    @property
+    def rows(self) -> tuple[int, int]:
+        return shard_rows(self.M, self.world, self.rank)
+
+    @property
+    def per_rank(self) -> int:
+        return -(-self.M // self.world)
+
+
+class RowShardedMulMat:
+    """dst = A·B with A's rows sharded over the process group.
+
+    Each rank passes its LOCAL shard a_local (ne=[K, rows owned]) and the replicated B.
+    ``compute(ga, a, b, dst)`` is the local operator (default: computeMatMul on the HIP
+    backend); the gather is ``torch.distributed.all_gather_into_tensor`` on ``group``.
+    """
+
+    def __init__(self, ga: GGMLGraphAllocator, M: int, N: int, world: int, rank: int, group=None, compute=None):
+        import torch
+        self.ga = ga
+        self.spec = ShardSpec(world, rank, M)
+        self.N = N
+        self.group = group
+        if compute is None:
+            from .ops import computeMatMul
+            compute = computeMatMul
+        self.compute = compute
+        dev = ga.buffers[0].device if hasattr(ga.buffers[0], "device") else "cpu"
+        per = self.spec.per_rank
+        # one contiguous gather buffer: rank r's slot holds rows [r*per, r*per+per) x N floats
+        self.gathered = torch.zeros(world * per * N, dtype=torch.float32, device=dev)
+        self.local = torch.zeros(per * N, dtype=torch.float32, device=dev)
+
+    def local_rows(self) -> tuple[int, int]:
+        return self.spec.rows
+
+    def forward(self, a_local: GGMLTensor, b: GGMLTensor, local_dst: GGMLTensor):
+        """Compute the local rows into local_dst (ne=[N, rows owned]) then all-gather.
+        Returns the full [M, N] float32 result (a view of the gather buffer)."""
+        import torch
+        import torch.distributed as dist
+        r0, r1 = self.spec.rows
+        if r1 > r0:
+            self.compute(self.ga, self.ga.context, a_local, b, local_dst)
+        n_local = (r1 - r0) * self.N
+        src = self.ga.buffers[local_dst.bufferId]
+        if isinstance(src, torch.Tensor):
+            flat = src[local_dst.dataOffset:local_dst.dataOffset + 4 * n_local].view(torch.float32)
+        else:
+            import numpy as np
+            flat = torch.from_numpy(np.frombuffer(src[local_dst.dataOffset:local_dst.dataOffset + 4 * n_local].tobytes(),
+                                                  np.float32).copy())
+        self.local.zero_()
+        self.local[:n_local].copy_(flat)
+        if self.spec.world > 1:
+            dist.all_gather_into_tensor(self.gathered, self.local, group=self.group)
+        else:
+            self.gathered.copy_(self.local)
+        return self.gathered[: self.spec.M * self.N].view(self.spec.M, self.N)

@@ -1,0 +1,274 @@
+"""GPU parity: the HIP backend (through the C-ABI) against the oracle on the same inputs.
+
+Bar (BASELINE.json north_star): F32 results within 1e-3 relative —
+normwise ||g-r||_inf/||r||_inf <= 1e-3 and per element |g-r| <= 1e-3*max(|r|, 1e-3*||r||_inf)
+(_util.parity_ok) — and bit-exact bytes for dequantize/quantize.
+"""
+import numpy as np
+import pytest
+
+from _util import parity_ok, pattern_f32, pattern_src, random_acts, random_weights
+
+pytestmark = pytest.mark.gpu
+
+Q_TYPES = [2, 3, 6]  # Q4_0, Q4_1, Q8_0 (lk_type ids)
+QNAME = {2: "Q4_0", 3: "Q4_1", 6: "Q8_0"}
+
+
+def make_inputs(O, qt, M, K, N, kind="random", seed=0):
+    if kind == "pattern":
+        src = pattern_src(qt, M * K, 42) * np.float32(0.25)
+        x = pattern_f32(K * N, 84).reshape(K, N)
+    else:
+        src = random_weights(M * K, 0x5EED + seed)
+        x = random_acts(K * N, 0x5EED + 1000 + seed).reshape(K, N)
+    if (M * K) % 32:
+        raise ValueError("quantizeTensor needs numElements % 32 == 0")
+    q = O.quantize(qt, src)
+    return q, x
+
+
+def gpu_matmul(qt, q, M, K, N, x, a_off=0, b_off=0, d_off=0, dst_row_pad=0, b_stride=None, host=False):
+    """Run computeMatMul through the ggml_hip mirror; returns dst as [M, N] float32."""
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="host" if host else "cuda", defaultBufferSize=16)
+    a_bytes = q.size
+    bcol = N if b_stride is None else b_stride
+    b_bytes = 4 * K * bcol
+    d_row = N + dst_row_pad
+    d_bytes = 4 * M * d_row
+    ia = ga.addBuffer(a_off + a_bytes + 64)
+    ib = ga.addBuffer(b_off + b_bytes + 64)
+    idd = ga.addBuffer(d_off + d_bytes + 64)
+    a = G.GGMLTensor(G.GGMLType(qt), [K, M, 1, 1], bufferId=ia, dataOffset=a_off, name="a")
+    b = G.GGMLTensor(G.GGMLType.F32, [N, K, 1, 1], nb=[4, 4 * bcol, 4 * bcol * K, 4 * bcol * K],
+                     bufferId=ib, dataOffset=b_off, name="b")
+    d = G.GGMLTensor(G.GGMLType.F32, [N, M, 1, 1], nb=[4, 4 * d_row, 4 * d_row * M, 4 * d_row * M],
+                     bufferId=idd, dataOffset=d_off, name="dst")
+    ga.setTensorBytes(a, q)
+    xb = np.zeros((K, bcol), np.float32)
+    xb[:, :N] = x
+    ga.setTensorBytes(b, xb.view(np.uint8).reshape(-1))
+    G.computeMatMul(ga, ga.context, a, b, d)
+    raw = ga.buffers[idd]
+    raw = raw if isinstance(raw, np.ndarray) else raw.cpu().numpy()
+    out = raw[d_off:d_off + d_bytes].view(np.float32).reshape(M, d_row)[:, :N]
+    return np.ascontiguousarray(out)
+
+
+SHAPES = [
+    (64, 64, 1),      # fast GEMV, one pair per lane
+    (256, 4096, 1),   # fast GEMV, full tiles
+    (100, 4096, 1),   # partial last tile
+    (37, 11008, 1),   # 172 pairs per row: ragged lane loop
+    (16, 96, 1),      # K % 64 != 0 -> generic kernel
+    (8, 40, 1),       # K % 32 != 0: blocks straddle rows (flat-index semantics)
+    (32, 128, 3),     # N > 1
+    (5, 256, 7),
+]
+
+
+@pytest.mark.parametrize("qt", Q_TYPES, ids=lambda t: QNAME[t])
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("kind", ["random", "pattern"])
+def test_mul_mat_vs_oracle(gpu, oracle, qt, shape, kind):
+    M, K, N = shape
+    q, x = make_inputs(oracle, qt, M, K, N, kind)
+    ref = oracle.mat_mul_q(qt, q, M, K, x)
+    got = gpu_matmul(qt, q, M, K, N, x)
+    ok, msg = parity_ok(got, ref)
+    assert ok, msg
+
+
+@pytest.mark.parametrize("qt", Q_TYPES, ids=lambda t: QNAME[t])
+def test_offsets_strides_and_host_path(gpu, oracle, qt):
+    M, K, N = 48, 256, 1
+    q, x = make_inputs(oracle, qt, M, K, N, seed=3)
+    ref = oracle.mat_mul_q(qt, q, M, K, x)
+    for kw in [dict(a_off=16, b_off=32, d_off=48), dict(a_off=2), dict(b_off=4), dict(dst_row_pad=3),
+               dict(b_stride=2), dict(host=True), dict(host=True, a_off=16, dst_row_pad=1)]:
+        got = gpu_matmul(qt, q, M, K, N, x, **kw)
+        ok, msg = parity_ok(got, ref)
+        assert ok, (kw, msg)
+
+
+def test_empty_and_k0(gpu, oracle):
+    import ggml_hip as G
+    # M = 0 and N = 0: nothing read or written
+    for (M, N) in [(0, 1), (4, 0)]:
+        ga = G.GGMLGraphAllocator(defaultBufferSize=1024)
+        a = ga.allocateTensor(G.GGMLType.Q4_0, [64, M])
+        b = ga.allocateTensor(G.GGMLType.F32, [N, 64])
+        d = ga.allocateTensor(G.GGMLType.F32, [N, M])
+        G.computeMatMul(ga, ga.context, a, b, d)
+    # K = 0: every dot product is the empty sum -> dst := 0 (GGMLComputeOps.kt:132-144 with no iterations)
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1024)
+    a = ga.allocateTensor(G.GGMLType.Q8_0, [0, 3])
+    b = ga.allocateTensor(G.GGMLType.F32, [2, 0])
+    d = ga.allocateTensor(G.GGMLType.F32, [2, 3])
+    ga.buffers[0].fill_(0xFF)
+    G.computeMatMul(ga, ga.context, a, b, d)
+    out = ga.buffers[0][d.dataOffset:d.dataOffset + 24].cpu().numpy().view(np.float32)
+    assert np.all(out == 0)
+
+
+def test_errors_raise_like_kotlin(gpu, oracle):
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 16)
+    a = ga.allocateTensor(G.GGMLType.Q4_0, [64, 4])
+    b = ga.allocateTensor(G.GGMLType.F32, [1, 64])
+    d = ga.allocateTensor(G.GGMLType.F32, [1, 4])
+    with pytest.raises(G.IllegalArgumentException):
+        G.computeMatMul(ga, ga.context, a, ga.allocateTensor(G.GGMLType.F32, [1, 32]), d)
+    with pytest.raises(G.IllegalArgumentException):
+        G.computeMatMul(ga, ga.context, a, b, ga.allocateTensor(G.GGMLType.F16, [1, 4]))
+    with pytest.raises(NotImplementedError):
+        G.computeMatMul(ga, ga.context, ga.allocateTensor(G.GGMLType.I32, [64, 4]),
+                        ga.allocateTensor(G.GGMLType.I32, [1, 64]), ga.allocateTensor(G.GGMLType.I32, [1, 4]))
+    bad = G.GGMLTensor(G.GGMLType.Q4_0, [64, 4], bufferId=0, dataOffset=ga.bufferSize(0) - 8)
+    with pytest.raises(G.IndexOutOfBoundsException):
+        G.computeMatMul(ga, ga.context, bad, b, d)
+    missing = G.GGMLTensor(G.GGMLType.Q4_0, [64, 4], bufferId=7)
+    with pytest.raises(G.IllegalStateException):
+        G.computeMatMul(ga, ga.context, missing, b, d)
+
+
+def test_f32_and_f16_general_path(gpu, oracle):
+    """General fallback (GGMLComputeOps.kt:1530-1556) on the device."""
+    O = oracle
+    import ggml_hip as G
+    for (M, K, N) in [(2, 3, 2), (4, 4, 4), (33, 70, 5), (64, 512, 64)]:
+        a = pattern_f32(M * K, 1)
+        x = pattern_f32(K * N, 2)
+        ref = O.mat_mul_q(O.F32, a.view(np.uint8), M, K, x.reshape(K, N))
+        ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 20)
+        ta = ga.allocateTensor(G.GGMLType.F32, [K, M]); ga.setTensorBytes(ta, a)
+        tb = ga.allocateTensor(G.GGMLType.F32, [N, K]); ga.setTensorBytes(tb, x)
+        td = ga.allocateTensor(G.GGMLType.F32, [N, M])
+        G.computeMatMul(ga, ga.context, ta, tb, td)
+        got = ga.tensorBytes(td).cpu().numpy().view(np.float32).reshape(M, N)
+        ok, msg = parity_ok(got, ref)
+        assert ok, msg
+    # F16 x F16 -> F16 (sum in f32, stored through Kotlin floatToHalf)
+    M, K, N = 12, 40, 3
+    ah = (pattern_f32(M * K, 5) * np.float32(0.1)).astype(np.float16)
+    bh = (pattern_f32(K * N, 6) * np.float32(0.1)).astype(np.float16)
+    abuf, bbuf = ah.view(np.uint8).copy(), bh.view(np.uint8).copy()
+    dbuf = np.zeros(M * N * 2, np.uint8)
+    st = O.compute_mat_mul(O.make_tensor(O.F16, [K, M], abuf), O.make_tensor(O.F16, [N, K], bbuf),
+                           O.make_tensor(O.F16, [N, M], dbuf))
+    assert st == 0
+    ref = dbuf.view(np.float16).astype(np.float32).reshape(M, N)
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 16)
+    ta = ga.allocateTensor(G.GGMLType.F16, [K, M]); ga.setTensorBytes(ta, abuf)
+    tb = ga.allocateTensor(G.GGMLType.F16, [N, K]); ga.setTensorBytes(tb, bbuf)
+    td = ga.allocateTensor(G.GGMLType.F16, [N, M])
+    G.computeMatMul(ga, ga.context, ta, tb, td)
+    got = ga.tensorBytes(td).cpu().numpy().view(np.float16).astype(np.float32).reshape(M, N)
+    np.testing.assert_allclose(got, ref, rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("qt", Q_TYPES, ids=lambda t: QNAME[t])
+def test_dequantize_bit_exact(gpu, oracle, qt):
+    import torch
+    import ggml_hip as G
+    n = 32 * 4096
+    src = random_weights(n, 11) * np.float32(50.0)
+    src[:64] = 0.0
+    src[64:96] = np.float32(1e-7)
+    q = oracle.quantize(qt, src)
+    ga = G.GGMLGraphAllocator(defaultBufferSize=q.size + 64)
+    t = ga.allocateTensor(G.GGMLType(qt), [n])
+    ga.setTensorBytes(t, q)
+    got = G.dequantizeTensor(ga, t).cpu().numpy()
+    torch.cuda.synchronize()
+    ref = oracle.dequantize(qt, q, n)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("qt", Q_TYPES, ids=lambda t: QNAME[t])
+def test_quantize_bit_exact(gpu, oracle, qt):
+    import torch
+    import ggml_hip as G
+    rng = np.random.default_rng(7)
+    parts = [random_weights(32 * 512, 3), random_acts(32 * 512, 4) * np.float32(1e3),
+             np.zeros(64, np.float32), np.full(32, 1e-30, np.float32),
+             (rng.standard_normal(32 * 64) * np.exp2(rng.uniform(-30, 10, 32 * 64))).astype(np.float32),
+             np.repeat(np.float32([0.5, -0.5, 1.5, 2.5]), 8)]
+    x = np.concatenate(parts).astype(np.float32)
+    ref = oracle.quantize(qt, x)
+    got = G.quantizeTensor(torch.from_numpy(x).cuda(), G.GGMLType(qt)).cpu().numpy()
+    assert np.array_equal(got, ref)
+
+
+def test_plan_equals_single_launches(gpu, oracle):
+    """Independent MUL_MAT nodes in one grouped launch give the same bits as one launch each."""
+    import torch
+    import ggml_hip as G
+    O = oracle
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 24)
+    nodes, refs = [], []
+    for i, (qt, M, K) in enumerate([(2, 96, 256), (2, 40, 512), (3, 64, 256), (6, 16, 1024), (2, 8, 96)]):
+        q, x = make_inputs(O, qt, M, K, 1, seed=20 + i)
+        a = ga.allocateTensor(G.GGMLType(qt), [K, M]); ga.setTensorBytes(a, q)
+        b = ga.allocateTensor(G.GGMLType.F32, [1, K]); ga.setTensorBytes(b, x)
+        d = ga.allocateTensor(G.GGMLType.F32, [1, M])
+        nodes.append((a, b, d))
+        refs.append(O.mat_mul_q(qt, q, M, K, x))
+    plan = G.MulMatPlan(ga, nodes)
+    assert plan.numLaunches == 4  # Q4_0 group (fast-path nodes), Q4_1, Q8_0, + the K=96 generic node
+    plan.launch()
+    torch.cuda.synchronize()
+    grouped = [ga.tensorBytes(d).cpu().numpy().view(np.float32).copy() for (_, _, d) in nodes]
+    for (a, b, d) in nodes:
+        G.computeMatMul(ga, ga.context, a, b, d)
+    torch.cuda.synchronize()
+    for (a, b, d), gr, ref in zip(nodes, grouped, refs):
+        single = ga.tensorBytes(d).cpu().numpy().view(np.float32)
+        assert np.array_equal(gr.view(np.uint32), single.view(np.uint32))
+        ok, msg = parity_ok(single.reshape(-1, 1), ref)
+        assert ok, msg
+
+
+def test_backend_graph_compute(gpu, oracle):
+    import ggml_hip as G
+    O = oracle
+    be = G.GGMLBackendRegistry.initBackend("HIP")
+    assert be.getName() == "HIP"
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 20)
+    q, x = make_inputs(O, 2, 64, 128, 1)
+    a = ga.allocateTensor(G.GGMLType.Q4_0, [128, 64]); ga.setTensorBytes(a, q)
+    b = ga.allocateTensor(G.GGMLType.F32, [1, 128]); ga.setTensorBytes(b, x)
+    d = ga.allocateTensor(G.GGMLType.F32, [1, 64])
+    d.op, d.src = G.GGMLOp.MUL_MAT, [a, b]
+    assert be.supportsOp(d)
+    assert be.graphCompute(G.GGMLCGraph([d], ga)) == G.GGMLStatus.SUCCESS
+    be.synchronize()
+    ok, msg = parity_ok(ga.tensorBytes(d).cpu().numpy().view(np.float32).reshape(64, 1), O.mat_mul_q(2, q, 64, 128, x))
+    assert ok, msg
+    bad = G.GGMLTensor(G.GGMLType.F32, [1, 64], op=G.GGMLOp.MUL_MAT, src=[a, ga.allocateTensor(G.GGMLType.F32, [1, 64])])
+    bad.bufferId = 0
+    assert be.graphCompute(G.GGMLCGraph([bad], ga)) == G.GGMLStatus.FAILED
+
+
+@pytest.mark.parametrize("qt,M,K", [(6, 4096, 4096), (2, 11008, 4096), (2, 4096, 11008), (3, 11008, 4096),
+                                    (2, 4096, 4096)])
+def test_full_size_batch1_vs_oracle(gpu, oracle, qt, M, K):
+    """BASELINE configs C2/C3 and the Q4_0 4096^2 headline shape at full size, N = 1."""
+    q, x = make_inputs(oracle, qt, M, K, 1, seed=M + K)
+    ref = oracle.mat_mul_q(qt, q, M, K, x, tight=True)
+    got = gpu_matmul(qt, q, M, K, 1, x)
+    ok, msg = parity_ok(got, ref)
+    assert ok, msg
+
+
+def test_full_size_linearity(gpu, oracle):
+    """Size-independent property: A(x1 + x2) == A x1 + A x2 (within the F32 bar)."""
+    qt, M, K = 2, 11008, 4096
+    q, x1 = make_inputs(oracle, qt, M, K, 1, seed=1)
+    x2 = random_acts(K, 99).reshape(K, 1)
+    y1 = gpu_matmul(qt, q, M, K, 1, x1)
+    y2 = gpu_matmul(qt, q, M, K, 1, x2)
+    y12 = gpu_matmul(qt, q, M, K, 1, (x1 + x2).astype(np.float32))
+    ok, msg = parity_ok(y12, (y1.astype(np.float64) + y2))
+    assert ok, msg
