@@ -46,10 +46,39 @@ def to_lk(ga: GGMLGraphAllocator, t: GGMLTensor) -> _lib.LkTensor:
     return lt
 
 
-def _stream_handle(stream=None) -> int | None:
-    import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return int(s.cuda_stream)
+_side_streams: dict = {}
+
+
+class _OnStream:
+    """Pick the HIP stream a launch goes to, ordered with torch's work.
+
+    An explicit (non-default) stream is used as is. When the caller is on torch's default
+    stream (handle 0), the launch goes to a library-owned side stream fenced both ways with
+    events (side waits for the caller's queue, the caller's queue waits for the launch):
+    on the GPU box, launches from this library onto the null stream were observed to be
+    unordered with torch's own null-stream copies (tools/diag3.py: stale dst reads)."""
+
+    def __init__(self, stream=None):
+        import torch
+        self.caller = stream if stream is not None else torch.cuda.current_stream()
+        if int(self.caller.cuda_stream) != 0:
+            self.stream, self.fence = self.caller, False
+        else:
+            dev = self.caller.device
+            key = dev.index if dev.index is not None else torch.cuda.current_device()
+            if key not in _side_streams:
+                _side_streams[key] = torch.cuda.Stream(device=dev)
+            self.stream, self.fence = _side_streams[key], True
+
+    def __enter__(self):
+        if self.fence:
+            self.stream.wait_stream(self.caller)
+        return int(self.stream.cuda_stream)
+
+    def __exit__(self, *exc):
+        if self.fence:
+            self.caller.wait_stream(self.stream)
+        return False
 
 
 def computeMatMul(graphAllocator: GGMLGraphAllocator, context: GGMLContext | None, a: GGMLTensor, b: GGMLTensor,
@@ -61,7 +90,8 @@ def computeMatMul(graphAllocator: GGMLGraphAllocator, context: GGMLContext | Non
     if all(host):
         st = L.lk_mul_mat(ctypes.byref(la), ctypes.byref(lb), ctypes.byref(ld))
     elif not any(host):
-        st = L.lk_mul_mat_device(ctypes.byref(la), ctypes.byref(lb), ctypes.byref(ld), _stream_handle(stream))
+        with _OnStream(stream) as sh:
+            st = L.lk_mul_mat_device(ctypes.byref(la), ctypes.byref(lb), ctypes.byref(ld), sh)
     else:
         raise _lib.IllegalArgumentException("operands must all be host or all be device buffers")
     _lib.check(st)
@@ -96,7 +126,8 @@ class MulMatPlan:
         return _lib.load().lk_plan_num_launches(self._handle)
 
     def launch(self, stream=None):
-        _lib.check(_lib.load().lk_plan_launch(self._handle, _stream_handle(stream)))
+        with _OnStream(stream) as sh:
+            _lib.check(_lib.load().lk_plan_launch(self._handle, sh))
 
     def close(self):
         if self._handle:
@@ -117,8 +148,8 @@ def dequantizeTensor(graphAllocator: GGMLGraphAllocator, tensor: GGMLTensor, str
     L = _lib.load()
     n = tensor.getNumBlocks() * 32
     out = torch.empty(n, dtype=torch.float32, device=graphAllocator.buffers[tensor.bufferId].device)
-    _lib.check(L.lk_dequantize_device(ctypes.byref(to_lk(graphAllocator, tensor)), ctypes.c_void_p(out.data_ptr()),
-                                      _stream_handle(stream)))
+    with _OnStream(stream) as sh:
+        _lib.check(L.lk_dequantize_device(ctypes.byref(to_lk(graphAllocator, tensor)), ctypes.c_void_p(out.data_ptr()), sh))
     return out
 
 
@@ -133,8 +164,9 @@ def quantizeTensor(src, targetType: GGMLType, stream=None):
     n = src.numel()
     bs = GGMLType(targetType).byteSize
     out = torch.empty((n // 32) * bs if n % 32 == 0 else 0, dtype=torch.uint8, device=src.device)
-    _lib.check(L.lk_quantize_device(ctypes.c_void_p(src.data_ptr()), n, int(targetType),
-                                    ctypes.c_void_p(out.data_ptr() if out.numel() else 0), _stream_handle(stream)))
+    with _OnStream(stream) as sh:
+        _lib.check(L.lk_quantize_device(ctypes.c_void_p(src.data_ptr()), n, int(targetType),
+                                        ctypes.c_void_p(out.data_ptr() if out.numel() else 0), sh))
     return out
 
 
