@@ -7,13 +7,22 @@ weights (llama.kotlin block layout), F32 activations, F32 outputs — 224 comput
 nodes, 3.65 GB of weights (> the 256 MiB Infinity Cache, so every step streams HBM).
 Weights are random-init N(0, 0.02^2) quantized on device; activations N(0, 1); synthetic.
 
-Multi-GPU (one process per GPU, RCCL): every weight matrix is row-sharded; rank r
-computes its rows of the 7 outputs of a layer in ONE grouped launch, then an RCCL
-all-gather (on a separate stream, overlapping the next layer) reassembles the layer's
-outputs on every rank. Total work per step is fixed -> "scaling": "strong".
+Schedule of the timed step: the synthetic activations make the 7 matmuls of a layer
+independent nodes, so each layer is two grouped launches (MulMatPlan): the six K=4096
+matrices (one-unit rows) and the K=11008 down projection (three-unit rows). The whole
+step is captured once in a HIP graph and replayed (no per-launch host overhead).
+A second line, "decode_chain", times the dependent schedule a real decode has —
+per layer {q,k,v} -> o -> {gate,up} -> down, 4 launches in stream order — on one GPU.
+
+Multi-GPU (one process per GPU, RCCL): every weight matrix is row-sharded; after each
+layer rank r all-gathers its rows of the layer's outputs on a separate stream that
+overlaps the next layer. Total work per step is fixed -> "scaling": "strong".
 
 value = whole-job algorithmic GB/s = Σ_nodes (M·K/32·18 + 4·K + 4·M) bytes per token x
 tokens / wall time (max over ranks). tokens_per_s is reported beside it.
+roofline = the dominant kernel (gemv_stream_kernel<Q4_0,1>, the six-matrix launch of each
+layer): its algorithmic bytes per launch / its average launch duration, from HIP events on
+the launch stream around each launch of one eager pass over the 32 layers.
 """
 import argparse
 import json
@@ -28,6 +37,10 @@ HIDDEN, FFN, LAYERS = 4096, 11008, 32
 # (name, M rows, K) — LlamaConfig defaults, K/model/LlamaModel.kt:8-21; shapes :159-195, :287-304
 LAYER_MATS = [("q", HIDDEN, HIDDEN), ("k", HIDDEN, HIDDEN), ("v", HIDDEN, HIDDEN), ("o", HIDDEN, HIDDEN),
               ("gate", FFN, HIDDEN), ("up", FFN, HIDDEN), ("down", HIDDEN, FFN)]
+# activation each matrix reads: q,k,v share the normed hidden state, gate/up the second one
+X_OF = {"q": "h", "k": "h", "v": "h", "o": "attn", "gate": "h2", "up": "h2", "down": "ffn"}
+X_LEN = {"h": HIDDEN, "attn": HIDDEN, "h2": HIDDEN, "ffn": FFN}
+CHAIN = [("q", "k", "v"), ("o",), ("gate", "up"), ("down",)]
 Q4_0_BLOCK = 18
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -42,6 +55,19 @@ def shard(M, world, rank):
     return r0, min(r0 + per, M)
 
 
+def capture(torch, fn, stream):
+    """HIP graph of fn() on `stream`; None when capture is refused (then fn runs eagerly)."""
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g, stream=stream):
+            fn()
+    except Exception as e:  # noqa: BLE001 — reported in the JSON line, eager fallback
+        print(f"[bench] graph capture failed ({type(e).__name__}: {e}); timing eager launches", file=sys.stderr)
+        torch.cuda.synchronize()
+        return None
+    return g
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -50,10 +76,11 @@ def main():
     ap.add_argument("--layers", type=int, default=LAYERS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-headline", action="store_true")
+    ap.add_argument("--no-chain", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=6144)
     args = ap.parse_args()
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -79,19 +106,26 @@ def main():
         for (name, M, K) in LAYER_MATS:
             r0, r1 = shard(M, world, rank)
             row.append((name, M, K, r0, r1))
-            w_bytes += (r1 - r0) * K // 32 * Q4_0_BLOCK
+            w_bytes += ((r1 - r0) * K // 32 * Q4_0_BLOCK + 15) // 16 * 16
         mats.append(row)
-    out_per_layer_local = sum(r1 - r0 for (_, _, _, r0, r1) in mats[0])
     out_per_layer_padded = sum(-(-M // world) for (_, M, _) in LAYER_MATS)
+    x_per_layer = sum(X_LEN.values())
     ga = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
     wbuf = ga.addBuffer(w_bytes + 256)          # all Q4_0 weight shards, back to back
-    xbuf = ga.addBuffer(4 * (HIDDEN + FFN) * args.layers + 256)
+    xbuf = ga.addBuffer(4 * x_per_layer * args.layers + 256)
     obuf = ga.addBuffer(4 * out_per_layer_padded * args.layers + 256)
-    woff = xoff = 0
-    plans, layer_nodes = [], []
+    woff = 0
+    nodes_by_layer = []  # per layer: {name: (a, b, d)}
     gathered = []
     for layer in range(args.layers):
-        nodes = []
+        xoff, xo = 4 * x_per_layer * layer, {}
+        for key, n in X_LEN.items():
+            xo[key] = xoff
+            xoff += 4 * n
+        xs = torch.randn(x_per_layer, generator=gen, device=dev)
+        base = 4 * x_per_layer * layer
+        ga.buffers[xbuf][base:base + 4 * x_per_layer].copy_(xs.view(torch.uint8))
+        nodes = {}
         ooff = 4 * out_per_layer_padded * layer
         for (name, M, K, r0, r1) in mats[layer]:
             rows = r1 - r0
@@ -103,18 +137,17 @@ def main():
                 ga.buffers[wbuf][woff:woff + nb].copy_(q)
                 del src, q
             woff += (nb + 15) // 16 * 16
-            b = G.GGMLTensor(T.F32, [1, K], bufferId=xbuf, dataOffset=xoff + (0 if K == HIDDEN else 4 * HIDDEN))
+            b = G.GGMLTensor(T.F32, [1, K], bufferId=xbuf, dataOffset=xo[X_OF[name]])
             d = G.GGMLTensor(T.F32, [1, rows], bufferId=obuf, dataOffset=ooff)
             ooff += 4 * -(-M // world)
-            nodes.append((a, b, d))
-        xs = torch.randn(HIDDEN + FFN, generator=gen, device=dev)
-        ga.buffers[xbuf][xoff:xoff + 4 * (HIDDEN + FFN)].copy_(xs.view(torch.uint8))
-        xoff += 4 * (HIDDEN + FFN)
-        layer_nodes.append(nodes)
-        plans.append(G.MulMatPlan(ga, nodes))
+            nodes[name] = (a, b, d)
+        nodes_by_layer.append(nodes)
         if world > 1:
             gathered.append(torch.empty(world * out_per_layer_padded, dtype=torch.float32, device=dev))
-    launches_per_step = sum(p.numLaunches for p in plans)
+    # timed schedule: per layer the six K=4096 matrices, then down
+    plans = [[G.MulMatPlan(ga, [n[k] for k in ("q", "k", "v", "o", "gate", "up")]), G.MulMatPlan(ga, [n["down"]])]
+             for n in nodes_by_layer]
+    launches_per_step = sum(p.numLaunches for lp in plans for p in lp)
     torch.cuda.synchronize()
 
     compute = torch.cuda.Stream(device=dev)
@@ -123,33 +156,40 @@ def main():
 
     def step():
         works = []
-        with torch.cuda.stream(compute):
-            for layer, plan in enumerate(plans):
+        for layer, lp in enumerate(plans):
+            for plan in lp:
                 plan.launch(stream=compute)
-                if world > 1:
-                    ev = torch.cuda.Event()
-                    ev.record(compute)
-                    comm.wait_event(ev)
-                    with torch.cuda.stream(comm):
-                        src = obuf_f32[out_per_layer_padded * layer: out_per_layer_padded * (layer + 1)]
-                        works.append(dist.all_gather_into_tensor(gathered[layer], src, async_op=True))
-        for w in works:
-            w.wait()
+            if world > 1:
+                ev = torch.cuda.Event()
+                ev.record(compute)
+                comm.wait_event(ev)
+                with torch.cuda.stream(comm):
+                    src = obuf_f32[out_per_layer_padded * layer: out_per_layer_padded * (layer + 1)]
+                    works.append(dist.all_gather_into_tensor(gathered[layer], src, async_op=True))
         if world > 1:
+            for w in works:
+                w.wait()
             compute.wait_stream(comm)
 
-    for _ in range(args.warmup):
-        step()
+    with torch.cuda.stream(compute):
+        for _ in range(args.warmup):
+            step()
+    torch.cuda.synchronize()
+    graph = None if args.no_graph else capture(torch, step, compute)
+    run = graph.replay if graph is not None else step
+    with torch.cuda.stream(compute):
+        run()  # one untimed replay (graph upload)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(compute)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    ev1.record(compute)
+    with torch.cuda.stream(compute):
+        ev0.record(compute)
+        for _ in range(args.steps):
+            run()
+        ev1.record(compute)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -165,12 +205,8 @@ def main():
     tokens = args.steps
     value_gbs = token_bytes * tokens / elapsed / 1e9
     ms_per_step = elapsed * 1e3 / args.steps
-    # dominant kernel (grouped Q4_0 GEMV, one launch per layer on this rank): algorithmic bytes per
-    # launch / average launch duration from HIP events on the launch stream over the timed region
-    local_layer_bytes = sum((r1 - r0) * K // 32 * Q4_0_BLOCK + 4 * K + 4 * (r1 - r0)
-                            for (_, M, K, r0, r1) in mats[0])
-    avg_launch_s = ev_ms / 1e3 / (args.steps * launches_per_step)
-    achieved = local_layer_bytes / avg_launch_s / 1e9
+
+    roof = roofline(torch, plans, mats, compute)
 
     result = {
         "metric": "Q4_0 matmul GB/s + tokens/sec 7B, 1/2/4/8 MI355X vs Kotlin CPU",
@@ -188,16 +224,17 @@ def main():
         "data": "synthetic (random-init N(0,0.02^2) weights quantized on device, N(0,1) activations)",
         "config": {"workload": "llama7b_token_matmuls_q4_0_n1", "layers": args.layers,
                    "matmuls_per_layer": len(LAYER_MATS), "global_batch": 1, "seq_len": 1,
-                   "bytes_per_token": token_bytes, "parallelism": f"row-shard{world}+rccl-allgather" if world > 1 else "single",
-                   "launches_per_step_per_rank": launches_per_step},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "gemv_q_n1_kernel<Q4_0> (grouped, 7 nodes per launch)",
-                     "bytes_per_launch": local_layer_bytes, "avg_launch_us": round(avg_launch_s * 1e6, 3)},
+                   "bytes_per_token": token_bytes,
+                   "parallelism": f"row-shard{world}+rccl-allgather" if world > 1 else "single",
+                   "launches_per_step_per_rank": launches_per_step, "hip_graph": graph is not None,
+                   "gpu_ms_per_step": round(ev_ms / args.steps, 4)},
+        "roofline": roof,
     }
 
+    if rank == 0 and world == 1 and not args.no_chain:
+        result["decode_chain"] = decode_chain(torch, G, ga, nodes_by_layer, compute, token_bytes)
     if rank == 0 and world == 1 and not args.no_headline:
-        result["headline_q4_0_4096x4096_n1"] = headline(G, ga, dev)
+        result["headline_q4_0_4096x4096_n1"] = headline(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, token_bytes)
     if rank == 0:
@@ -207,10 +244,64 @@ def main():
         dist.destroy_process_group()
 
 
-def headline(G, ga, dev, copies=48, reps=20):
-    """North-star shape: Q4_0 4096x4096, N=1, single computeMatMul per launch, rotating over
-    `copies` distinct weight matrices (48 x 9.4 MB = 453 MB > 256 MiB Infinity Cache)."""
-    import torch
+def roofline(torch, plans, mats, stream, reps=3):
+    """Dominant kernel: the six-matrix K=4096 launch of each layer. HIP events on the launch
+    stream around every such launch of `reps` eager passes over all layers (distinct weights per
+    layer, so each launch streams HBM); achieved = algorithmic bytes per launch / mean duration."""
+    pairs = []
+    with torch.cuda.stream(stream):
+        for _ in range(reps):
+            for lp in plans:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                lp[0].launch(stream=stream)
+                e1.record(stream)
+                pairs.append((e0, e1))
+    torch.cuda.synchronize()
+    avg_s = sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) / 1e3
+    nbytes = sum((r1 - r0) * K // 32 * Q4_0_BLOCK + 4 * K + 4 * (r1 - r0)
+                 for (name, M, K, r0, r1) in mats[0] if name != "down")
+    achieved = nbytes / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "gemv_stream_kernel<Q4_0,1> (q,k,v,o,gate,up of one layer in one launch)",
+            "bytes_per_launch": nbytes, "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": len(pairs)}
+
+
+def decode_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, reps=20):
+    """Dependent decode schedule on one GPU: per layer {q,k,v} -> o -> {gate,up} -> down,
+    4 stream-ordered launches (128 per token), captured in a HIP graph."""
+    plans = [[G.MulMatPlan(ga, [n[k] for k in grp]) for grp in CHAIN] for n in nodes_by_layer]
+
+    def token():
+        for lp in plans:
+            for p in lp:
+                p.launch(stream=stream)
+
+    with torch.cuda.stream(stream):
+        token()
+    torch.cuda.synchronize()
+    g = capture(torch, token, stream)
+    run = g.replay if g is not None else token
+    with torch.cuda.stream(stream):
+        run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            run()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    per = e0.elapsed_time(e1) / 1e3 / reps
+    return {"tokens_per_s": round(1 / per, 2), "ms_per_token": round(per * 1e3, 4),
+            "achieved_GBps": round(token_bytes / per / 1e9, 1), "launches_per_token": 4 * len(plans),
+            "hip_graph": g is not None, "tokens_timed": reps}
+
+
+def headline(torch, G, dev, copies=48, reps=20):
+    """North-star shape: Q4_0 4096x4096, N=1, rotating over `copies` distinct weight matrices
+    (48 x 9.4 MB = 453 MB > 256 MiB Infinity Cache). Two numbers: one computeMatMul launch per
+    matrix (graph-replayed, so launch-bound by the kernel itself, not the host), and the 48
+    matrices as one grouped launch (MulMatPlan)."""
     T = G.GGMLType
     M = K = 4096
     nb = M * K // 32 * Q4_0_BLOCK
@@ -225,21 +316,37 @@ def headline(G, ga, dev, copies=48, reps=20):
     nodes = [(G.GGMLTensor(T.Q4_0, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [1, K], bufferId=xb),
               G.GGMLTensor(T.F32, [1, M], bufferId=db, dataOffset=4 * M * c)) for c in range(copies)]
     s = torch.cuda.Stream(device=dev)
+
+    def singles():
+        for (a, b, d) in nodes:
+            G.computeMatMul(g, None, a, b, d, stream=s)
+
+    plan = G.MulMatPlan(g, nodes)
+
+    def timed(fn, n_launch):
+        with torch.cuda.stream(s):
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
+                fn()
+            e1.record(s)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / (reps * n_launch)
+
     with torch.cuda.stream(s):
-        for _ in range(2):
-            for (a, b, d) in nodes:
-                G.computeMatMul(g, None, a, b, d, stream=s)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(reps):
-            for (a, b, d) in nodes:
-                G.computeMatMul(g, None, a, b, d, stream=s)
-        e1.record(s)
+        singles()
     torch.cuda.synchronize()
-    per = e0.elapsed_time(e1) / 1e3 / (reps * copies)
+    gr = capture(torch, singles, s)
+    per = timed(gr.replay if gr is not None else singles, copies)
+    per_grouped = timed(lambda: plan.launch(stream=s), 1)
     gbs = alg_bytes(M, K) / per / 1e9
+    gbs_g = copies * alg_bytes(M, K) / per_grouped / 1e9
     return {"launches": reps * copies, "avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(gbs, 1),
-            "frac_of_8TBps": round(gbs / HBM_PEAK_GBS, 4), "rotating_weight_copies": copies}
+            "frac_of_8TBps": round(gbs / HBM_PEAK_GBS, 4), "hip_graph": gr is not None,
+            "rotating_weight_copies": copies,
+            "grouped_48_in_one_launch": {"avg_launch_us": round(per_grouped * 1e6, 3), "achieved_GBps": round(gbs_g, 1),
+                                         "frac_of_8TBps": round(gbs_g / HBM_PEAK_GBS, 4)}}
 
 
 def cpu_baseline(sample_rows, token_bytes):

@@ -218,14 +218,64 @@ GemvDesc make_desc(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
   return d;
 }
 
-int launch_gemv_group(int32_t qt, const GemvDesc &single, const GemvDesc *ddescs, const uint16_t *dmap, int ntiles,
-                      hipStream_t st) {
+// LDS-DMA streaming kernel eligibility on top of gemv_eligible: at most kStreamMaxUnits
+// units of 64 block pairs per row, rows a whole number of 16-byte DMA lanes, A 16-aligned.
+// Returns the units-per-row class (1..kStreamMaxUnits) or 0.
+int stream_class(const lk_tensor *a, const Checked &c) {
+  const int64_t np = c.K / 64;
+  const int64_t nch = (np + 63) / 64;
+  if (nch < 1 || nch > kStreamMaxUnits) return 0;
+  if ((np * 2 * block_bytes(a->type)) % 16) return 0;
+  if (((uintptr_t)a->data + a->data_offset) % 16) return 0;
+  return (int)nch;
+}
+
+int cu_count() {
+  static int cached[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+template <int QT, int CPL>
+void launch_stream_t(int grid, const GemvDesc &single, const StreamWork *work, int spw, hipStream_t st) {
+  constexpr size_t lds = StreamGeom<QT, CPL>::LDS;
+  hipLaunchKernelGGL((gemv_stream_kernel<QT, CPL>), dim3(grid), dim3(kStreamWaves * 64), lds, st, single, work, spw);
+}
+
+int launch_stream(int32_t qt, int cpl, int grid, const GemvDesc &single, const StreamWork *work, int spw,
+                  hipStream_t st) {
+  if (grid <= 0) return LK_OK;
+#define LK_STREAM(T, C) \
+  if (qt == T && cpl == C) { launch_stream_t<T, C>(grid, single, work, spw, st); HIP_TRY(hipGetLastError()); return LK_OK; }
+  LK_STREAM(LK_TYPE_Q4_0, 1) LK_STREAM(LK_TYPE_Q4_0, 2) LK_STREAM(LK_TYPE_Q4_0, 3)
+  LK_STREAM(LK_TYPE_Q4_1, 1) LK_STREAM(LK_TYPE_Q4_1, 2) LK_STREAM(LK_TYPE_Q4_1, 3)
+  LK_STREAM(LK_TYPE_Q8_0, 1) LK_STREAM(LK_TYPE_Q8_0, 2) LK_STREAM(LK_TYPE_Q8_0, 3)
+#undef LK_STREAM
+  return fail(LK_ERR_NOT_IMPLEMENTED, "stream gemv: type %d class %d", qt, cpl);
+}
+
+// Workgroups for `rows` rows: one per CU, but no fewer than ~kStreamWaves rows each.
+int stream_grid(int64_t rows) {
+  const int64_t g = (rows + kStreamWaves - 1) / kStreamWaves;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cu_count()));
+}
+
+int launch_gemv_v1(int32_t qt, const GemvDesc &d, hipStream_t st) {
+  const int rpt = kGemvWaves * rows_per_wave(qt);
+  const int64_t ntiles = ((int64_t)d.M + rpt - 1) / rpt;
   if (ntiles <= 0) return LK_OK;
-  dim3 grid(ntiles), block(256);
+  if (ntiles > INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "too many rows");
+  dim3 grid((unsigned)ntiles), block(256);
   switch (qt) {
-    case LK_TYPE_Q4_0: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q4_0, kRowsQ4>), grid, block, 0, st, single, ddescs, dmap); break;
-    case LK_TYPE_Q4_1: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q4_1, kRowsQ4>), grid, block, 0, st, single, ddescs, dmap); break;
-    case LK_TYPE_Q8_0: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q8_0, kRowsQ8>), grid, block, 0, st, single, ddescs, dmap); break;
+    case LK_TYPE_Q4_0: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q4_0, kRowsQ4>), grid, block, 0, st, d); break;
+    case LK_TYPE_Q4_1: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q4_1, kRowsQ4>), grid, block, 0, st, d); break;
+    case LK_TYPE_Q8_0: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q8_0, kRowsQ8>), grid, block, 0, st, d); break;
     default: return fail(LK_ERR_NOT_IMPLEMENTED, "gemv: type %d", qt);
   }
   HIP_TRY(hipGetLastError());
@@ -261,12 +311,10 @@ int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const
 // Single eligible GEMV: the descriptor travels in the kernel arguments (no
 // allocation, no host sync: stream-ordered and graph-capturable).
 int run_single_gemv(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
-  const int rows_per_tile = kGemvWaves * rows_per_wave(a->type);
-  const int64_t ntiles = (c.M + rows_per_tile - 1) / rows_per_tile;
-  if (ntiles > INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "too many rows");
-  GemvDesc d = make_desc(a, b, dst, c);
-  d.tile_begin = 0;
-  return launch_gemv_group(a->type, d, nullptr, nullptr, (int)ntiles, st);
+  const GemvDesc d = make_desc(a, b, dst, c);
+  if (const int cls = stream_class(a, c))
+    return launch_stream(a->type, cls, stream_grid(c.M), d, nullptr, 0, st);
+  return launch_gemv_v1(a->type, d, st);
 }
 
 int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
@@ -436,57 +484,98 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   return LK_OK;
 }
 
-// ---- plans: independent MUL_MAT nodes, one grouped launch per quant type ----------
+// ---- plans: independent MUL_MAT nodes, one launch per (quant type, units-per-row class) ----
+//
+// Stream-eligible nodes of one class share a launch: the concatenated rows are split
+// into one contiguous, byte-balanced range per workgroup (one workgroup per CU), cut at
+// node boundaries into segments.
 
 struct lk_plan {
-  struct Group { int32_t qt; int ntiles; void *dev; const GemvDesc *descs; const uint16_t *map; };
+  struct Group { int32_t qt; int cls; int grid; int spw; StreamWork *work; };
   std::vector<Group> groups;
   struct Single { lk_tensor a, b, d; Checked c; };
   std::vector<Single> singles;
 };
+
+namespace {
+
+// Workgroup g gets global rows [bound[g], bound[g+1]) of the concatenation of descs,
+// balanced by weight bytes, cut at node boundaries into work slots (spw per workgroup).
+void build_work(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<StreamWork> &work, int *spw) {
+  const int64_t pb = 2 * block_bytes(qt);
+  const size_t n = descs.size();
+  std::vector<int64_t> row0(n + 1, 0), byte0(n + 1, 0);
+  for (size_t i = 0; i < n; i++) {
+    row0[i + 1] = row0[i] + descs[i].M;
+    byte0[i + 1] = byte0[i] + (int64_t)descs[i].M * (descs[i].K / 64) * pb;
+  }
+  const int64_t total = byte0[n];
+  std::vector<int64_t> bound(grid + 1);
+  for (int g = 0; g <= grid; g++) {
+    const int64_t target = (int64_t)((__int128)total * g / grid);
+    size_t i = 0;
+    while (i + 1 < n && byte0[i + 1] <= target) i++;
+    const int64_t rb = (descs[i].K / 64) * pb;
+    int64_t r = rb ? (target - byte0[i] + rb - 1) / rb : 0;
+    r = std::min<int64_t>(std::max<int64_t>(r, 0), descs[i].M);
+    bound[g] = (g == grid) ? row0[n] : row0[i] + r;
+  }
+  std::vector<std::vector<StreamWork>> per(grid);
+  size_t most = 1;
+  for (int g = 0; g < grid; g++) {
+    for (size_t i = 0; i < n; i++) {
+      const int64_t lo = std::max(bound[g], row0[i]), hi = std::min(bound[g + 1], row0[i + 1]);
+      if (lo >= hi) continue;
+      StreamWork w{};
+      w.a = descs[i].a; w.x = descs[i].x; w.dst = descs[i].dst; w.dst_row_stride = descs[i].dst_row_stride;
+      w.K = descs[i].K; w.row_begin = (int32_t)(lo - row0[i]); w.row_end = (int32_t)(hi - row0[i]);
+      per[g].push_back(w);
+    }
+    most = std::max(most, per[g].size());
+  }
+  *spw = (int)most;
+  work.assign((size_t)grid * most, StreamWork{});
+  for (int g = 0; g < grid; g++) {
+    for (size_t k = 0; k < per[g].size(); k++) work[(size_t)g * most + k] = per[g][k];
+    work[(size_t)g * most].count = (int32_t)per[g].size();
+  }
+}
+
+}  // namespace
 
 int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n, lk_plan **out) {
   if (!out || n < 0) return fail(LK_ERR_INVALID_ARG, "bad plan arguments");
   int rc = ensure_init();
   if (rc) return rc;
   auto plan = new lk_plan();
-  std::map<int32_t, std::vector<GemvDesc>> by_type;
-  std::map<int32_t, int64_t> tiles;
+  std::map<std::pair<int32_t, int>, std::vector<GemvDesc>> by_class;
   for (int i = 0; i < n; i++) {
     Checked c;
     rc = check(&a[i], &b[i], &dst[i], &c);
-    if (rc) { delete plan; return rc; }
+    if (rc) { lk_plan_destroy(plan); return rc; }
     if (c.empty) continue;
-    if (gemv_eligible(&a[i], &b[i], &dst[i], c)) {
-      GemvDesc d = make_desc(&a[i], &b[i], &dst[i], c);
-      const int rpt = kGemvWaves * rows_per_wave(a[i].type);
-      d.tile_begin = (int32_t)tiles[a[i].type];
-      tiles[a[i].type] += (c.M + rpt - 1) / rpt;
-      by_type[a[i].type].push_back(d);
-    } else {
-      plan->singles.push_back({a[i], b[i], dst[i], c});
-    }
+    const int cls = gemv_eligible(&a[i], &b[i], &dst[i], c) ? stream_class(&a[i], c) : 0;
+    if (cls) by_class[{a[i].type, cls}].push_back(make_desc(&a[i], &b[i], &dst[i], c));
+    else plan->singles.push_back({a[i], b[i], dst[i], c});
   }
-  for (auto &kv : by_type) {
-    const int32_t qt = kv.first;
+  for (auto &kv : by_class) {
+    const int32_t qt = kv.first.first;
+    const int cls = kv.first.second;
     auto &descs = kv.second;
-    const int64_t nt = tiles[qt];
-    if (nt > INT32_MAX || descs.size() > 65535) { delete plan; return fail(LK_ERR_NOT_IMPLEMENTED, "plan too large"); }
-    std::vector<uint16_t> map((size_t)nt);
-    for (size_t di = 0; di < descs.size(); di++) {
-      int64_t end = (di + 1 < descs.size()) ? descs[di + 1].tile_begin : nt;
-      for (int64_t t = descs[di].tile_begin; t < end; t++) map[(size_t)t] = (uint16_t)di;
-    }
-    const size_t db = descs.size() * sizeof(GemvDesc), mb = map.size() * sizeof(uint16_t);
+    int64_t rows = 0;
+    for (auto &d : descs) rows += d.M;
+    const int grid = stream_grid(rows);
+    std::vector<StreamWork> work;
+    int spw = 1;
+    build_work(descs, qt, grid, work, &spw);
     void *dev = nullptr;
-    if (hipMalloc(&dev, db + mb) != hipSuccess) { delete plan; return fail(LK_ERR_DEVICE, "plan alloc"); }
-    if (hipMemcpy(dev, descs.data(), db, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy((uint8_t *)dev + db, map.data(), mb, hipMemcpyHostToDevice) != hipSuccess) {
-      (void)hipFree(dev);
-      delete plan;
+    const size_t wb = work.size() * sizeof(StreamWork);
+    if (hipMalloc(&dev, wb) != hipSuccess) { lk_plan_destroy(plan); return fail(LK_ERR_DEVICE, "plan alloc"); }
+    plan->groups.push_back({qt, cls, grid, spw, (StreamWork *)dev});
+    if (hipMemcpy(dev, work.data(), wb, hipMemcpyHostToDevice) != hipSuccess) {
+      lk_plan_destroy(plan);
       return fail(LK_ERR_DEVICE, "plan upload");
     }
-    plan->groups.push_back({qt, (int)nt, dev, (const GemvDesc *)dev, (const uint16_t *)((uint8_t *)dev + db)});
   }
   *out = plan;
   return LK_OK;
@@ -496,7 +585,7 @@ int lk_plan_launch(lk_plan *plan, void *stream) {
   if (!plan) return fail(LK_ERR_INVALID_ARG, "null plan");
   hipStream_t st = pick_stream(stream);
   for (auto &g : plan->groups) {
-    int rc = launch_gemv_group(g.qt, GemvDesc{}, g.descs, g.map, g.ntiles, st);
+    int rc = launch_stream(g.qt, g.cls, g.grid, GemvDesc{}, g.work, g.spw, st);
     if (rc) return rc;
   }
   for (auto &s : plan->singles) {
@@ -512,7 +601,7 @@ int lk_plan_num_launches(const lk_plan *plan) {
 
 void lk_plan_destroy(lk_plan *plan) {
   if (!plan) return;
-  for (auto &g : plan->groups) (void)hipFree(g.dev);
+  for (auto &g : plan->groups) (void)hipFree(g.work);
   delete plan;
 }
 

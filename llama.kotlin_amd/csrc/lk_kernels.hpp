@@ -175,46 +175,32 @@ __device__ __forceinline__ float pair_dot<LK_TYPE_Q8_0>(const uint32_t *w, const
   return fmaf(d1, fmaf(-128.f, xs1, u), acc);
 }
 
-// ---- grouped batch-1 GEMV (the hot kernel) ------------------------------------
+// ---- batch-1 GEMV ----------------------------------------------------------------
 
-// One MUL_MAT node of a grouped launch (device-resident operands).
+// One MUL_MAT node with N == 1 (device-resident operands).
 struct GemvDesc {
   const uint8_t *a;   // first byte of A's blocks (buffer base + dataOffset)
   const float *x;     // B column 0 (contiguous K floats)
   float *dst;         // dst(0, 0)
   int64_t dst_row_stride; // elements between dst(0,i) and dst(0,i+1) (= nb[1]/4)
   int32_t M, K;
-  int32_t tile_begin; // first workgroup tile of this node
-  int32_t pad;
 };
 
-constexpr int kGemvWaves = 4;  // waves per workgroup
+constexpr int kGemvWaves = 4;  // waves per workgroup of the register-streaming kernel
 
-// Grid: one workgroup per tile of kGemvWaves*ROWS rows of one node; tile_map[blockIdx.x]
-// names the node. Each wave owns ROWS consecutive rows; each lane owns block pairs
-// p = lane, lane+64, ... of those rows. Per pair the lane loads its 64 activations
-// once (float4, L1/L2-resident) and reuses them for all ROWS rows, whose 2·BB-byte
-// pairs it loads with dword-aligned vector loads (coalesced at wave level: 64 lanes
-// cover 64·2·BB contiguous bytes of a row).
+// Register-streaming GEMV: the path for batch-1 shapes the LDS-DMA kernel below does not
+// take (K > 12288, rows not 16-byte multiples). One workgroup per kGemvWaves*ROWS rows.
+// Each wave owns ROWS consecutive rows; each lane owns block pairs p = lane, lane+64, ...
+// of those rows. Per pair the lane loads its 64 activations once (float4, L1/L2-resident)
+// and reuses them for all ROWS rows, whose 2·BB-byte pairs it loads with dword-aligned
+// vector loads (coalesced at wave level: 64 lanes cover 64·2·BB contiguous bytes of a row).
 template <int QT, int ROWS>
-__global__ __launch_bounds__(256) void gemv_q_n1_kernel(const GemvDesc single, const GemvDesc *__restrict__ descs,
-                                                        const uint16_t *__restrict__ tile_map) {
+__global__ __launch_bounds__(256) void gemv_q_n1_kernel(const GemvDesc d) {
   constexpr int BB = QTraits<QT>::BB;
   constexpr int PDW = QTraits<QT>::PAIR_DW;
-  const int tile = blockIdx.x;
-  // single node: descriptor in kernel arguments; grouped: tile_map names the node
-  GemvDesc d = single;
-  if (tile_map) {
-    const int di = __builtin_amdgcn_readfirstlane(((const LK_GLOBAL uint16_t *)tile_map)[tile]);
-    const LK_GLOBAL uint64_t *src = (const LK_GLOBAL uint64_t *)(descs + di);
-    uint64_t words[sizeof(GemvDesc) / 8];
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(GemvDesc) / 8); i++) words[i] = src[i];
-    __builtin_memcpy(&d, words, sizeof(GemvDesc));
-  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int row0 = ((tile - d.tile_begin) * kGemvWaves + wave) * ROWS;
+  const int row0 = ((int)blockIdx.x * kGemvWaves + wave) * ROWS;
   if (row0 >= d.M) return;
   const int nrows = min(ROWS, d.M - row0);
   const int npairs = d.K >> 6;
@@ -253,6 +239,305 @@ __global__ __launch_bounds__(256) void gemv_q_n1_kernel(const GemvDesc single, c
   for (int r = 0; r < ROWS; r++) {
     float v = wave_sum(acc[r]);
     if (lane == 0 && r < nrows) ((LK_GLOBAL float *)d.dst)[(int64_t)(row0 + r) * d.dst_row_stride] = v;
+  }
+}
+
+// ---- LDS-DMA streaming GEMV (the hot kernel) -------------------------------------
+//
+// A batch-1 quantized GEMV moves ~0.56 (Q4_0) to ~1.06 (Q8_0) bytes of weights per
+// multiply-add, so it is bound by HBM. Keeping HBM busy takes ~40 KB of loads in flight
+// per CU; VGPR-destination loads cannot hold that much at useful occupancy. This kernel
+// puts the weight bytes in flight with global_load_lds (LDS-DMA: 1 KB per wave
+// instruction, no VGPRs) into a per-wave ring of D slots, and decodes from LDS.
+//
+// Work: a "unit" is 64 consecutive block pairs of one row (one pair per lane). A row of
+// K weights is nch = ceil(K/4096) units. A workgroup (kStreamWaves waves, one per CU)
+// processes a list of segments (node, row range); each wave takes a contiguous share of
+// a segment's rows and streams its units through its ring, D-1 units ahead, waiting
+// with a counted vmcnt. The activations of the segment's node are staged once into LDS
+// in the decode order and then held in VGPRs (16 float4 per unit of the row).
+//
+// Q4 decode: v_cvt_pk_f32_fp8 of a nibble n (exponent field 0/1) is exactly n·2^-9, so
+// one conversion turns two nibbles into two floats; the sums are rescaled by 512.
+// Q8 decode: bytes biased to unsigned (xor 0x80) go through v_cvt_f32_ubyteN.
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+#define LK_LDS __attribute__((address_space(3)))
+
+constexpr int kStreamWaves = 8;
+constexpr int kLdsBytes = 160 * 1024;
+constexpr int kStreamMaxUnits = 3;   // units per row held in VGPRs: K <= 12288
+
+// A workgroup's piece of one node: rows [row_begin, row_end) of the node, with the node's
+// operands inlined so a workgroup reaches its first weight load after one scalar load.
+// Workgroup g owns slots work[g*spw .. g*spw + work[g*spw].count).
+struct StreamWork {
+  const uint8_t *a;
+  const float *x;
+  float *dst;
+  int64_t dst_row_stride;
+  int32_t K, row_begin, row_end, count;
+  int64_t pad[2];
+};
+static_assert(sizeof(StreamWork) == 64, "one s_load_dwordx16");
+
+template <int QT, int CPL> struct StreamGeom {
+  static constexpr int PB = 2 * QTraits<QT>::BB;         // bytes per block pair
+  static constexpr int PDW = PB / 4;
+  static constexpr int UB = 64 * PB;                      // bytes per unit
+  static constexpr int L = (UB + 1023) / 1024;            // DMA instructions per unit
+  static constexpr int SLOT = L * 1024;
+  static constexpr int PITCH = 64 * CPL + 1;              // activation image pitch (float4)
+  static constexpr int IMG = 16 * PITCH * 16;
+  static constexpr int DFIT = (kLdsBytes - IMG) / (kStreamWaves * SLOT);
+  static constexpr int D = DFIT < 3 ? DFIT : 3;            // ring depth (units)
+  static constexpr int LDS = IMG + kStreamWaves * D * SLOT;
+  static constexpr int VMCNT = (D - 1) * L;               // DMA ops allowed in flight past the unit in use
+  static_assert(D >= 2, "ring must double-buffer");
+  static_assert(VMCNT < 64, "vmcnt field is 6 bits");
+};
+
+// s_waitcnt vmcnt(N) with the other counters left alone (gfx9 encoding).
+template <int N> __device__ __forceinline__ void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | 0x0F70);
+}
+__device__ __forceinline__ void wait_lgkmcnt0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
+template <bool HI> __device__ __forceinline__ f2v fp8x2(uint32_t v) { return __builtin_amdgcn_cvt_pk_f32_fp8(v, HI); }
+
+// Σ (n_k/512)·x_k over the 8 nibbles of dword u; xa = (x0,x2,x4,x6), xb = (x1,x3,x5,x7).
+__device__ __forceinline__ f2v nib8(uint32_t u, f32x4 xa, f32x4 xb, f2v s) {
+  const uint32_t lo = u & 0x0F0F0F0Fu, hi = (u >> 4) & 0x0F0F0F0Fu;
+  s = __builtin_elementwise_fma(fp8x2<false>(lo), f2v{xa.x, xa.y}, s);
+  s = __builtin_elementwise_fma(fp8x2<true>(lo), f2v{xa.z, xa.w}, s);
+  s = __builtin_elementwise_fma(fp8x2<false>(hi), f2v{xb.x, xb.y}, s);
+  s = __builtin_elementwise_fma(fp8x2<true>(hi), f2v{xb.z, xb.w}, s);
+  return s;
+}
+
+// Σ (q_k+128)·x_k over the 4 signed bytes of dword u; xv = (x0,x1,x2,x3).
+__device__ __forceinline__ f2v i8x4(uint32_t u, f32x4 xv, f2v s) {
+  const uint32_t b = u ^ 0x80808080u;
+  s = __builtin_elementwise_fma(f2v{(float)(b & 0xFF), (float)((b >> 8) & 0xFF)}, f2v{xv.x, xv.y}, s);
+  s = __builtin_elementwise_fma(f2v{(float)((b >> 16) & 0xFF), (float)(b >> 24)}, f2v{xv.z, xv.w}, s);
+  return s;
+}
+
+// One block pair (w = PDW dwords, LDS) against its 64 activations in decode order.
+template <int QT>
+__device__ __forceinline__ float pair_dot_s(const uint32_t *w, const f32x4 *xr, float xs0, float xs1);
+
+template <>
+__device__ __forceinline__ float pair_dot_s<LK_TYPE_Q4_0>(const uint32_t *w, const f32x4 *xr, float xs0, float xs1) {
+  // d0 = bytes 0..1, quants 2..17 (realigned by 2); d1 = bytes 18..19, quants 20..35
+  f2v s = {0.f, 0.f}, t = {0.f, 0.f};
+  s = nib8(align2(w[1], w[0]), xr[0], xr[1], s);
+  s = nib8(align2(w[2], w[1]), xr[2], xr[3], s);
+  s = nib8(align2(w[3], w[2]), xr[4], xr[5], s);
+  s = nib8(align2(w[4], w[3]), xr[6], xr[7], s);
+  t = nib8(w[5], xr[8], xr[9], t);
+  t = nib8(w[6], xr[10], xr[11], t);
+  t = nib8(w[7], xr[12], xr[13], t);
+  t = nib8(w[8], xr[14], xr[15], t);
+  const float acc = h2f(w[0]) * fmaf(512.f, s.x + s.y, -8.f * xs0);
+  return fmaf(h2f(w[4] >> 16), fmaf(512.f, t.x + t.y, -8.f * xs1), acc);
+}
+
+template <>
+__device__ __forceinline__ float pair_dot_s<LK_TYPE_Q4_1>(const uint32_t *w, const f32x4 *xr, float xs0, float xs1) {
+  // (d0,m0) = bytes 0..3, quants 4..19; (d1,m1) = 20..23, quants 24..39
+  f2v s = {0.f, 0.f}, t = {0.f, 0.f};
+  s = nib8(w[1], xr[0], xr[1], s);
+  s = nib8(w[2], xr[2], xr[3], s);
+  s = nib8(w[3], xr[4], xr[5], s);
+  s = nib8(w[4], xr[6], xr[7], s);
+  t = nib8(w[6], xr[8], xr[9], t);
+  t = nib8(w[7], xr[10], xr[11], t);
+  t = nib8(w[8], xr[12], xr[13], t);
+  t = nib8(w[9], xr[14], xr[15], t);
+  float acc = fmaf(h2f(w[0]), 512.f * (s.x + s.y), h2f(w[0] >> 16) * xs0);
+  acc = fmaf(h2f(w[5] >> 16), xs1, acc);
+  return fmaf(h2f(w[5]), 512.f * (t.x + t.y), acc);
+}
+
+template <>
+__device__ __forceinline__ float pair_dot_s<LK_TYPE_Q8_0>(const uint32_t *w, const f32x4 *xr, float xs0, float xs1) {
+  // d0 = bytes 0..1, q = 2..33 (realigned by 2); d1 = bytes 34..35, q = 36..67
+  f2v s = {0.f, 0.f}, t = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 8; k++) s = i8x4(align2(w[k + 1], w[k]), xr[k], s);
+#pragma unroll
+  for (int k = 0; k < 8; k++) t = i8x4(w[9 + k], xr[8 + k], t);
+  const float acc = h2f(w[0]) * fmaf(-128.f, xs0, s.x + s.y);
+  return fmaf(h2f(w[8] >> 16), fmaf(-128.f, xs1, t.x + t.y), acc);
+}
+
+// DPP reduction over the wave (VALU only); lane 63 ends with the total.
+__device__ __forceinline__ float dpp_sum(float v) {
+#define LK_DPP(ctrl, rmask, bc) \
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, rmask, 0xF, bc))
+  LK_DPP(0xB1, 0xF, true);    // quad_perm [1,0,3,2]
+  LK_DPP(0x4E, 0xF, true);    // quad_perm [2,3,0,1]
+  LK_DPP(0x141, 0xF, true);   // row_half_mirror
+  LK_DPP(0x140, 0xF, true);   // row_mirror
+  LK_DPP(0x142, 0xA, false);  // row_bcast:15
+  LK_DPP(0x143, 0xC, false);  // row_bcast:31
+#undef LK_DPP
+  return v;
+}
+
+// Grid: one workgroup per CU. work == nullptr: one node (`single`), rows split evenly
+// over the grid; otherwise workgroup g runs its slots of `work`.
+// Requirements (checked by the host): K % 64 == 0, ceil(K/4096) <= CPL, row bytes
+// (K/64·PB) % 16 == 0, A and x 16-byte aligned, x contiguous.
+template <int QT, int CPL>
+__global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const GemvDesc single,
+                                                                        const StreamWork *__restrict__ work, int spw) {
+  using G = StreamGeom<QT, CPL>;
+  extern __shared__ f32x4 lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint8_t *ring = (uint8_t *)(lds + 16 * G::PITCH) + wave * (G::D * G::SLOT);
+  const StreamWork *wk = work ? work + (int64_t)blockIdx.x * spw : nullptr;
+  const int nseg = wk ? ((const __attribute__((address_space(4))) int32_t *)wk)[offsetof(StreamWork, count) / 4] : 1;
+  for (int si = 0; si < nseg; si++) {
+    const uint8_t *a_node;
+    const float *x_node;
+    float *dst_node;
+    int64_t dst_stride;
+    int K, rb, re;
+    if (wk) {
+      StreamWork w;  // scalar loads (constant address space: the work list is never written)
+      {
+        const __attribute__((address_space(4))) uint64_t *src = (const __attribute__((address_space(4))) uint64_t *)(wk + si);
+        uint64_t words[sizeof(StreamWork) / 8];
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(StreamWork) / 8); i++) words[i] = src[i];
+        __builtin_memcpy(&w, words, sizeof(StreamWork));
+      }
+      a_node = w.a; x_node = w.x; dst_node = w.dst; dst_stride = w.dst_row_stride;
+      K = w.K; rb = w.row_begin; re = w.row_end;
+    } else {
+      a_node = single.a; x_node = single.x; dst_node = single.dst; dst_stride = single.dst_row_stride;
+      K = single.K;
+      const int per = (single.M + (int)gridDim.x - 1) / (int)gridDim.x;
+      rb = min((int)blockIdx.x * per, single.M);
+      re = min(rb + per, single.M);
+    }
+    const int per_w = (re - rb + kStreamWaves - 1) / kStreamWaves;
+    const int r0 = __builtin_amdgcn_readfirstlane(min(rb + wave * per_w, re));
+    const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + per_w, re) - r0);
+    const int NP = K >> 6;                         // block pairs per row
+    const int nch = (NP + 63) >> 6;                // units per row
+    const int64_t RB = (int64_t)NP * G::PB;        // row bytes
+    const int nunits = nrows * nch;
+    const LK_GLOBAL uint8_t *A = (const LK_GLOBAL uint8_t *)a_node + (int64_t)r0 * RB;
+
+    // 1. activations -> LDS image, slot t of pair p at lds[t*PITCH + p] in decode order.
+    //    Staged before the weight DMA is issued: LDS accesses behind pending LDS-DMA make the
+    //    compiler wait for the whole DMA (vmcnt(0)), so the image goes first.
+    const LK_GLOBAL f32x4 *xv = (const LK_GLOBAL f32x4 *)x_node;
+    const int nq = NP * 16;
+    f32x4 xg[2 * CPL];
+#pragma unroll
+    for (int i = 0; i < 2 * CPL; i++) xg[i] = xv[min(tid + i * kStreamWaves * 64, nq - 1)];
+    __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
+#pragma unroll
+    for (int i = 0; i < 2 * CPL; i++) {
+      const int q = tid + i * kStreamWaves * 64;
+      if (q < nq) {
+        const int p = q >> 4, t = q & 15;
+        const f32x4 v = xg[i];
+        if constexpr (QT == LK_TYPE_Q8_0) {
+          lds[t * G::PITCH + p] = v;  // natural order: slot t = x[4t .. 4t+3]
+        } else {
+          // slot 2j = (x0,x2,x4,x6), slot 2j+1 = (x1,x3,x5,x7) of x[8j .. 8j+7]
+          const int jj = t >> 1, h = t & 1;
+          ((f2v *)(lds + (2 * jj) * G::PITCH + p))[h] = f2v{v.x, v.z};
+          ((f2v *)(lds + (2 * jj + 1) * G::PITCH + p))[h] = f2v{v.y, v.w};
+        }
+      }
+    }
+
+    // 2. DMA prologue: exactly D units in flight; past the wave's last unit (or for a wave
+    //    without rows) the slots are filled from the node's first row and never decoded
+    int irow = 0, ich = 0, islot = 0, issued = 0;
+    auto dma_unit = [&](const LK_GLOBAL uint8_t *base, int ubytes, int sl) {
+      LK_LDS uint8_t *slot = (LK_LDS uint8_t *)(ring + sl * G::SLOT);
+#pragma unroll
+      for (int j = 0; j < G::L; j++) {
+        int off = j * 1024 + lane * 16;
+        off = off < ubytes ? off : 0;  // lanes past the unit re-read its first 16 B (never decoded)
+        __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + off), (LK_LDS void *)(slot + j * 1024), 16, 0, 0);
+      }
+    };
+    auto issue = [&]() {
+      dma_unit(A + (int64_t)irow * RB + (int64_t)ich * G::UB, (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB), islot);
+      if (++ich == nch) { ich = 0; ++irow; }
+      islot = (islot + 1 == G::D) ? 0 : islot + 1;
+      ++issued;
+    };
+#pragma unroll
+    for (int k = 0; k < G::D; k++) {
+      const bool real = k < nunits;
+      const LK_GLOBAL uint8_t *base = real ? A + (int64_t)irow * RB + (int64_t)ich * G::UB : (const LK_GLOBAL uint8_t *)a_node;
+      const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : (int)min((int64_t)G::UB, RB);
+      dma_unit(base, ubytes, k);
+      if (real) {
+        if (++ich == nch) { ich = 0; ++irow; }
+        ++issued;
+      }
+    }
+    islot = 0;  // the next unit to issue is unit D, slot D % D
+
+    wait_lgkmcnt0();
+    __builtin_amdgcn_s_barrier();
+    f32x4 xr[CPL][16];
+    float xs0[CPL], xs1[CPL];
+    bool valid[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; c++) {
+      const int p = c * 64 + lane;
+      valid[c] = p < NP;
+      const int pc = valid[c] ? p : 0;
+#pragma unroll
+      for (int t = 0; t < 16; t++) xr[c][t] = lds[t * G::PITCH + pc];
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        a0 += (xr[c][t].x + xr[c][t].y) + (xr[c][t].z + xr[c][t].w);
+        a1 += (xr[c][t + 8].x + xr[c][t + 8].y) + (xr[c][t + 8].z + xr[c][t + 8].w);
+      }
+      xs0[c] = a0;
+      xs1[c] = a1;
+    }
+
+    int slot = 0, u = 0;
+    LK_GLOBAL float *out = (LK_GLOBAL float *)dst_node + (int64_t)r0 * dst_stride;
+    for (int row = 0; row < nrows; row++) {
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPL; c++) {
+        if (c < nch) {
+          if (u + G::D - 1 < nunits) wait_vmcnt<G::VMCNT>();
+          else wait_vmcnt<0>();
+          const uint32_t *rp = (const uint32_t *)(ring + slot * G::SLOT + lane * G::PB);
+          uint32_t w[G::PDW];
+#pragma unroll
+          for (int k = 0; k < G::PDW; k++) w[k] = rp[k];
+          const float v = pair_dot_s<QT>(w, xr[c], xs0[c], xs1[c]);
+          acc += valid[c] ? v : 0.f;
+          if (issued < nunits) {
+            wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
+            issue();
+          }
+          slot = (slot + 1 == G::D) ? 0 : slot + 1;
+          ++u;
+        }
+      }
+      const float tot = dpp_sum(acc);
+      if (lane == 63) out[(int64_t)row * dst_stride] = tot;
+    }
   }
 }
 

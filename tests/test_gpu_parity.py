@@ -57,10 +57,13 @@ def gpu_matmul(qt, q, M, K, N, x, a_off=0, b_off=0, d_off=0, dst_row_pad=0, b_st
 
 
 SHAPES = [
-    (64, 64, 1),      # fast GEMV, one pair per lane
-    (256, 4096, 1),   # fast GEMV, full tiles
-    (100, 4096, 1),   # partial last tile
-    (37, 11008, 1),   # 172 pairs per row: ragged lane loop
+    (64, 64, 1),      # one pair per row: register-streaming GEMV (row bytes not a 16 B multiple)
+    (256, 4096, 1),   # LDS-DMA GEMV, one unit (64 pairs) per row
+    (100, 4096, 1),   # rows not a multiple of the waves
+    (37, 11008, 1),   # 172 pairs per row: three units, the last one partial
+    (70, 4352, 1),    # 68 pairs: two units, 4 pairs in the second
+    (9, 16384, 1),    # 256 pairs per row: beyond the LDS-DMA kernel's VGPR-held activations
+    (33, 320, 1),     # 5 pairs per row: odd pair count
     (16, 96, 1),      # K % 64 != 0 -> generic kernel
     (8, 40, 1),       # K % 32 != 0: blocks straddle rows (flat-index semantics)
     (32, 128, 3),     # N > 1
@@ -206,9 +209,10 @@ def test_plan_equals_single_launches(gpu, oracle):
     import torch
     import ggml_hip as G
     O = oracle
-    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 24)
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 26)
     nodes, refs = [], []
-    for i, (qt, M, K) in enumerate([(2, 96, 256), (2, 40, 512), (3, 64, 256), (6, 16, 1024), (2, 8, 96)]):
+    for i, (qt, M, K) in enumerate([(2, 96, 256), (2, 40, 512), (3, 64, 256), (6, 16, 1024), (2, 8, 96),
+                                    (2, 3000, 4096), (2, 5, 4096), (2, 700, 11008), (2, 1, 8192)]):
         q, x = make_inputs(O, qt, M, K, 1, seed=20 + i)
         a = ga.allocateTensor(G.GGMLType(qt), [K, M]); ga.setTensorBytes(a, q)
         b = ga.allocateTensor(G.GGMLType.F32, [1, K]); ga.setTensorBytes(b, x)
@@ -216,7 +220,9 @@ def test_plan_equals_single_launches(gpu, oracle):
         nodes.append((a, b, d))
         refs.append(O.mat_mul_q(qt, q, M, K, x))
     plan = G.MulMatPlan(ga, nodes)
-    assert plan.numLaunches == 4  # Q4_0 group (fast-path nodes), Q4_1, Q8_0, + the K=96 generic node
+    # launches: Q4_0 one-unit rows, Q4_0 two-unit rows (K=8192), Q4_0 three-unit rows (K=11008),
+    # Q4_1, Q8_0, + the K=96 generic node
+    assert plan.numLaunches == 6
     plan.launch()
     torch.cuda.synchronize()
     grouped = [ga.tensorBytes(d).cpu().numpy().view(np.float32).copy() for (_, _, d) in nodes]
