@@ -8,9 +8,8 @@ nodes, 3.65 GB of weights (> the 256 MiB Infinity Cache, so every step streams H
 Weights are random-init N(0, 0.02^2) quantized on device; activations N(0, 1); synthetic.
 
 Schedule of the timed step: the synthetic activations make the 7 matmuls of a layer
-independent nodes, so each layer is two grouped launches (MulMatPlan): the six K=4096
-matrices (one-unit rows) and the K=11008 down projection (three-unit rows). The whole
-step is captured once in a HIP graph and replayed (no per-launch host overhead).
+independent nodes, so each layer is one grouped launch (MulMatPlan). The whole step is
+captured once in a HIP graph and replayed (no per-launch host overhead).
 A second line, "decode_chain", times the dependent schedule a real decode has —
 per layer {q,k,v} -> o -> {gate,up} -> down, 4 launches in stream order — on one GPU.
 
@@ -20,9 +19,9 @@ overlaps the next layer. Total work per step is fixed -> "scaling"
 
 value = whole-job algorithmic GB/s = Σ_nodes (M·K/32·18 + 4·K + 4·M) bytes per token x
 tokens / wall time (max over ranks). tokens_per_s is reported beside it.
-roofline = the dominant kernel (gemv_stream_kernel<Q4_0,1>, the six-matrix launch of each
-layer): its algorithmic bytes per launch / its average launch duration, from HIP events on
-the launch stream around each launch of one eager pass over the 32 layers.
+roofline = the dominant (only) kernel of the step, gemv_stream_kernel<Q4_0,3>: algorithmic
+bytes per launch / average launch duration, from HIP events on the launch stream around
+graph replays of the 32 layer launches.
 """
 import argparse
 import json
@@ -144,9 +143,8 @@ def main():
         nodes_by_layer.append(nodes)
         if world > 1:
             gathered.append(torch.empty(world * out_per_layer_padded, dtype=torch.float32, device=dev))
-    # timed schedule: per layer the six K=4096 matrices, then down
-    plans = [[G.MulMatPlan(ga, [n[k] for k in ("q", "k", "v", "o", "gate", "up")]), G.MulMatPlan(ga, [n["down"]])]
-             for n in nodes_by_layer]
+    # timed schedule: per layer one grouped launch of its 7 matrices
+    plans = [[G.MulMatPlan(ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
     launches_per_step = sum(p.numLaunches for lp in plans for p in lp)
     torch.cuda.synchronize()
 
@@ -244,28 +242,49 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(torch, plans, mats, stream, reps=3):
-    """Dominant kernel: the six-matrix K=4096 launch of each layer. HIP events on the launch
-    stream around every such launch of `reps` eager passes over all layers (distinct weights per
-    layer, so each launch streams HBM); achieved = algorithmic bytes per launch / mean duration."""
-    pairs = []
+def roofline(torch, plans, mats, stream, reps=10):
+    """Dominant kernel: the grouped launch of each layer (all 7 matrices, gemv_stream_kernel<Q4_0,3>).
+    A HIP graph of the 32 layer launches (distinct weights per layer, so each launch streams HBM)
+    is replayed `reps` times between two events on the launch stream; the mean launch duration is
+    that time / launches (inter-launch gaps inside a graph are included, so this is a lower bound
+    on the kernel's own rate). achieved = algorithmic bytes per launch / mean duration."""
+    def layers():
+        for lp in plans:
+            lp[0].launch(stream=stream)
+
+    g = capture(torch, layers, stream)
+    run = g.replay if g is not None else layers
     with torch.cuda.stream(stream):
+        run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
         for _ in range(reps):
-            for lp in plans:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                lp[0].launch(stream=stream)
-                e1.record(stream)
-                pairs.append((e0, e1))
+            run()
+        e1.record(stream)
     torch.cuda.synchronize()
-    avg_s = sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) / 1e3
-    nbytes = sum((r1 - r0) * K // 32 * Q4_0_BLOCK + 4 * K + 4 * (r1 - r0)
-                 for (name, M, K, r0, r1) in mats[0] if name != "down")
+    n = reps * len(plans)
+    avg_s = e0.elapsed_time(e1) / 1e3 / n
+    nbytes = sum((r1 - r0) * K // 32 * Q4_0_BLOCK + 4 * K + 4 * (r1 - r0) for (name, M, K, r0, r1) in mats[0])
     achieved = nbytes / avg_s / 1e9
+    traffic, src = pmc_traffic("gemv_stream_kernel<2, 3>")
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "gemv_stream_kernel<Q4_0,1> (q,k,v,o,gate,up of one layer in one launch)",
-            "bytes_per_launch": nbytes, "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": len(pairs)}
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+            "kernel": "gemv_stream_kernel<Q4_0,3> (the 7 matrices of one layer in one launch)",
+            "bytes_per_launch": nbytes, "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": n,
+            "hip_graph": g is not None}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC profile of this bench
+    (profiles/rNN/traffic.json: FETCH_SIZE x 2 + WRITE_SIZE per launch, separate --pmc passes of
+    tools/profile.sh, summarised by tools/prof_summary.py); (None, None) when absent."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+        with open(f) as fh:
+            t = json.load(fh)
+        if kernel in t.get("kernel", ""):
+            return t["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
 
 
 def decode_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, reps=20):

@@ -484,7 +484,7 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   return LK_OK;
 }
 
-// ---- plans: independent MUL_MAT nodes, one launch per (quant type, units-per-row class) ----
+// ---- plans: independent MUL_MAT nodes, one launch per quant type ---------------------------
 //
 // Stream-eligible nodes of one class share a launch: the concatenated rows are split
 // into one contiguous, byte-balanced range per workgroup (one workgroup per CU), cut at
@@ -548,19 +548,25 @@ int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
   int rc = ensure_init();
   if (rc) return rc;
   auto plan = new lk_plan();
-  std::map<std::pair<int32_t, int>, std::vector<GemvDesc>> by_class;
+  // one launch per quant type: the kernel instance for the largest units-per-row class
+  // also runs the nodes with fewer units (same occupancy: 8 waves per CU either way)
+  std::map<int32_t, std::vector<GemvDesc>> by_type;
+  std::map<int32_t, int> type_cls;
   for (int i = 0; i < n; i++) {
     Checked c;
     rc = check(&a[i], &b[i], &dst[i], &c);
     if (rc) { lk_plan_destroy(plan); return rc; }
     if (c.empty) continue;
     const int cls = gemv_eligible(&a[i], &b[i], &dst[i], c) ? stream_class(&a[i], c) : 0;
-    if (cls) by_class[{a[i].type, cls}].push_back(make_desc(&a[i], &b[i], &dst[i], c));
+    if (cls) {
+      by_type[a[i].type].push_back(make_desc(&a[i], &b[i], &dst[i], c));
+      type_cls[a[i].type] = std::max(type_cls[a[i].type], cls);
+    }
     else plan->singles.push_back({a[i], b[i], dst[i], c});
   }
-  for (auto &kv : by_class) {
-    const int32_t qt = kv.first.first;
-    const int cls = kv.first.second;
+  for (auto &kv : by_type) {
+    const int32_t qt = kv.first;
+    const int cls = type_cls[qt];
     auto &descs = kv.second;
     int64_t rows = 0;
     for (auto &d : descs) rows += d.M;

@@ -264,6 +264,15 @@ __global__ __launch_bounds__(256) void gemv_q_n1_kernel(const GemvDesc d) {
 typedef float f2v __attribute__((ext_vector_type(2)));
 #define LK_LDS __attribute__((address_space(3)))
 
+// Cache policy (aux) of the weight stream's LDS-DMA: 2 = nt (bytes read once per launch).
+#ifndef LK_WEIGHT_AUX
+#define LK_WEIGHT_AUX 2
+#endif
+// Prologue order: 0 = activations then D weight units; 1 = weight unit 0, activations, units 1..D-1.
+#ifndef LK_PROLOGUE_ORDER
+#define LK_PROLOGUE_ORDER 0
+#endif
+
 constexpr int kStreamWaves = 8;
 constexpr int kLdsBytes = 160 * 1024;
 constexpr int kStreamMaxUnits = 3;   // units per row held in VGPRs: K <= 12288
@@ -287,8 +296,7 @@ template <int QT, int CPL> struct StreamGeom {
   static constexpr int UB = 64 * PB;                      // bytes per unit
   static constexpr int L = (UB + 1023) / 1024;            // DMA instructions per unit
   static constexpr int SLOT = L * 1024;
-  static constexpr int PITCH = 64 * CPL + 1;              // activation image pitch (float4)
-  static constexpr int IMG = 16 * PITCH * 16;
+  static constexpr int IMG = 64 * CPL * 256;              // activation image: 256 B per pair
   static constexpr int DFIT = (kLdsBytes - IMG) / (kStreamWaves * SLOT);
   static constexpr int D = DFIT < 3 ? DFIT : 3;            // ring depth (units)
   static constexpr int LDS = IMG + kStreamWaves * D * SLOT;
@@ -386,6 +394,19 @@ __device__ __forceinline__ float dpp_sum(float v) {
   return v;
 }
 
+// Optional per-wave timeline (tools/lab/trace.hip defines LK_STREAM_TRACE): s_memrealtime
+// (100 MHz) at kernel entry, activations in VGPRs, first unit decoded, and exit.
+#ifdef LK_STREAM_TRACE
+__device__ uint64_t *lk_trace_buf;
+#define LK_TRACE(slot)                                                                                  \
+  do {                                                                                                  \
+    if (lane == 0 && lk_trace_buf)                                                                      \
+      lk_trace_buf[((size_t)blockIdx.x * kStreamWaves + wave) * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LK_TRACE(slot) do {} while (0)
+#endif
+
 // Grid: one workgroup per CU. work == nullptr: one node (`single`), rows split evenly
 // over the grid; otherwise workgroup g runs its slots of `work`.
 // Requirements (checked by the host): K % 64 == 0, ceil(K/4096) <= CPL, row bytes
@@ -397,7 +418,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
   extern __shared__ f32x4 lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint8_t *ring = (uint8_t *)(lds + 16 * G::PITCH) + wave * (G::D * G::SLOT);
+  uint8_t *ring = (uint8_t *)lds + G::IMG + wave * (G::D * G::SLOT);
+  LK_TRACE(0);
   const StreamWork *wk = work ? work + (int64_t)blockIdx.x * spw : nullptr;
   const int nseg = wk ? ((const __attribute__((address_space(4))) int32_t *)wk)[offsetof(StreamWork, count) / 4] : 1;
   for (int si = 0; si < nseg; si++) {
@@ -433,34 +455,15 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     const int nunits = nrows * nch;
     const LK_GLOBAL uint8_t *A = (const LK_GLOBAL uint8_t *)a_node + (int64_t)r0 * RB;
 
-    // 1. activations -> LDS image, slot t of pair p at lds[t*PITCH + p] in decode order.
-    //    Staged before the weight DMA is issued: LDS accesses behind pending LDS-DMA make the
-    //    compiler wait for the whole DMA (vmcnt(0)), so the image goes first.
-    const LK_GLOBAL f32x4 *xv = (const LK_GLOBAL f32x4 *)x_node;
-    const int nq = NP * 16;
-    f32x4 xg[2 * CPL];
-#pragma unroll
-    for (int i = 0; i < 2 * CPL; i++) xg[i] = xv[min(tid + i * kStreamWaves * 64, nq - 1)];
-    __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
-#pragma unroll
-    for (int i = 0; i < 2 * CPL; i++) {
-      const int q = tid + i * kStreamWaves * 64;
-      if (q < nq) {
-        const int p = q >> 4, t = q & 15;
-        const f32x4 v = xg[i];
-        if constexpr (QT == LK_TYPE_Q8_0) {
-          lds[t * G::PITCH + p] = v;  // natural order: slot t = x[4t .. 4t+3]
-        } else {
-          // slot 2j = (x0,x2,x4,x6), slot 2j+1 = (x1,x3,x5,x7) of x[8j .. 8j+7]
-          const int jj = t >> 1, h = t & 1;
-          ((f2v *)(lds + (2 * jj) * G::PITCH + p))[h] = f2v{v.x, v.z};
-          ((f2v *)(lds + (2 * jj + 1) * G::PITCH + p))[h] = f2v{v.y, v.w};
-        }
-      }
-    }
-
-    // 2. DMA prologue: exactly D units in flight; past the wave's last unit (or for a wave
-    //    without rows) the slots are filled from the node's first row and never decoded
+    // 1. prologue, all by LDS-DMA:
+    //    - weights: exactly D units in flight; past the wave's last unit (or for a wave
+    //      without rows) the slots are filled from the node's first row and never decoded;
+    //    - the activation image: float4 t (x[4t..4t+3]) of pair p at lds[16p + (t ^ (p & 15))]
+    //      (XOR swizzle: each DMA instruction reads 1 KB of x contiguously, and the per-lane
+    //      reads below hit 64 distinct banks); image float4 i = 64·k + lane comes from DMA
+    //      instruction k, issued by wave k % 8.
+    //    LK_PROLOGUE_ORDER 1 issues weight unit 0 first, then the image, then units 1..D-1:
+    //    the HBM stream starts at once and the wait for the image covers unit 0 too.
     int irow = 0, ich = 0, islot = 0, issued = 0;
     auto dma_unit = [&](const LK_GLOBAL uint8_t *base, int ubytes, int sl) {
       LK_LDS uint8_t *slot = (LK_LDS uint8_t *)(ring + sl * G::SLOT);
@@ -468,7 +471,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       for (int j = 0; j < G::L; j++) {
         int off = j * 1024 + lane * 16;
         off = off < ubytes ? off : 0;  // lanes past the unit re-read its first 16 B (never decoded)
-        __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + off), (LK_LDS void *)(slot + j * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + off), (LK_LDS void *)(slot + j * 1024), 16, 0,
+                                         LK_WEIGHT_AUX);
       }
     };
     auto issue = [&]() {
@@ -477,8 +481,20 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       islot = (islot + 1 == G::D) ? 0 : islot + 1;
       ++issued;
     };
+    auto dma_x = [&]() {
+      const LK_GLOBAL f32x4 *xv = (const LK_GLOBAL f32x4 *)x_node;
+      const int ninst = (NP + 3) / 4;  // 64 float4 per instruction
+      for (int k = wave; k < ninst; k += kStreamWaves) {
+        const int i = k * 64 + lane;          // image position
+        const int p = min(i >> 4, NP - 1), t = (i & 15) ^ ((i >> 4) & 15);  // past the last pair: never read
+        __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(xv + p * 16 + t), (LK_LDS void *)(lds + k * 64), 16, 0, 0);
+      }
+    };
+    __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
+    if (LK_PROLOGUE_ORDER == 0) dma_x();
 #pragma unroll
     for (int k = 0; k < G::D; k++) {
+      if (LK_PROLOGUE_ORDER == 1 && k == 1) dma_x();
       const bool real = k < nunits;
       const LK_GLOBAL uint8_t *base = real ? A + (int64_t)irow * RB + (int64_t)ich * G::UB : (const LK_GLOBAL uint8_t *)a_node;
       const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : (int)min((int64_t)G::UB, RB);
@@ -490,8 +506,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     }
     islot = 0;  // the next unit to issue is unit D, slot D % D
 
-    wait_lgkmcnt0();
-    __builtin_amdgcn_s_barrier();
+    wait_vmcnt<(LK_PROLOGUE_ORDER == 0 ? G::D : G::D - 1) * G::L>();  // this wave's activation DMA has landed
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+
+    // 2. activations into VGPRs in decode order, and Σx per block
     f32x4 xr[CPL][16];
     float xs0[CPL], xs1[CPL];
     bool valid[CPL];
@@ -501,7 +519,16 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       valid[c] = p < NP;
       const int pc = valid[c] ? p : 0;
 #pragma unroll
-      for (int t = 0; t < 16; t++) xr[c][t] = lds[t * G::PITCH + pc];
+      for (int jj = 0; jj < 8; jj++) {
+        const f32x4 n0 = lds[16 * pc + ((2 * jj) ^ (pc & 15))], n1 = lds[16 * pc + ((2 * jj + 1) ^ (pc & 15))];
+        if constexpr (QT == LK_TYPE_Q8_0) {
+          xr[c][2 * jj] = n0;
+          xr[c][2 * jj + 1] = n1;
+        } else {  // nibble order: (x0,x2,x4,x6), (x1,x3,x5,x7)
+          xr[c][2 * jj] = f32x4{n0.x, n0.z, n1.x, n1.z};
+          xr[c][2 * jj + 1] = f32x4{n0.y, n0.w, n1.y, n1.w};
+        }
+      }
       float a0 = 0.f, a1 = 0.f;
 #pragma unroll
       for (int t = 0; t < 8; t++) {
@@ -512,6 +539,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       xs1[c] = a1;
     }
 
+    if (si == 0) LK_TRACE(1);
     int slot = 0, u = 0;
     LK_GLOBAL float *out = (LK_GLOBAL float *)dst_node + (int64_t)r0 * dst_stride;
     for (int row = 0; row < nrows; row++) {
@@ -535,10 +563,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
           ++u;
         }
       }
+      if (si == 0 && row == 0) LK_TRACE(2);
       const float tot = dpp_sum(acc);
       if (lane == 63) out[(int64_t)row * dst_stride] = tot;
     }
   }
+  LK_TRACE(3);
 }
 
 // ---- generic path (any K, any byte strides, ragged blocks) ----------------------

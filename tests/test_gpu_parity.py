@@ -64,6 +64,7 @@ SHAPES = [
     (70, 4352, 1),    # 68 pairs: two units, 4 pairs in the second
     (9, 16384, 1),    # 256 pairs per row: beyond the LDS-DMA kernel's VGPR-held activations
     (33, 320, 1),     # 5 pairs per row: odd pair count
+    (17, 384, 1),     # 6 pairs per row (Q4_1 streams it: rows of 240 B)
     (16, 96, 1),      # K % 64 != 0 -> generic kernel
     (8, 40, 1),       # K % 32 != 0: blocks straddle rows (flat-index semantics)
     (32, 128, 3),     # N > 1
@@ -220,9 +221,8 @@ def test_plan_equals_single_launches(gpu, oracle):
         nodes.append((a, b, d))
         refs.append(O.mat_mul_q(qt, q, M, K, x))
     plan = G.MulMatPlan(ga, nodes)
-    # launches: Q4_0 one-unit rows, Q4_0 two-unit rows (K=8192), Q4_0 three-unit rows (K=11008),
-    # Q4_1, Q8_0, + the K=96 generic node
-    assert plan.numLaunches == 6
+    # launches: Q4_0 (one-, two- and three-unit rows together), Q4_1, Q8_0, + the K=96 generic node
+    assert plan.numLaunches == 4
     plan.launch()
     torch.cuda.synchronize()
     grouped = [ga.tensorBytes(d).cpu().numpy().view(np.float32).copy() for (_, _, d) in nodes]
