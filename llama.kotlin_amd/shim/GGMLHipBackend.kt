@@ -1,0 +1,127 @@
+// GGMLHipBackend.kt — the reference-side binding a maintainer adds to llama.kotlin
+// (src/nativeMain/kotlin/ai/solace/llamakotlin/core/), over the cinterop of include/lk_hip.h.
+//
+// It implements the reference's GGMLBackend plugin interface (K/core/GGMLBackend.kt:90-157)
+// for exactly one op: MUL_MAT with src0 in {Q4_0, Q4_1, Q8_0} (or F32/F16 general) and F32
+// activations, keeping the host ByteArrays authoritative (K/core/GGMLAlloc.kt:271). Every
+// other node is left to GGMLCpuBackend. Not compiled in this repository (no Kotlin/Native
+// toolchain offline); it is the integration contract the C-ABI tests in tests/test_abi.py pin.
+package ai.solace.llamakotlin.core
+
+import ai.solace.llamakotlin.hip.*
+import kotlinx.cinterop.*
+
+/** lk_status -> the exception computeMatMul throws (K/core/GGMLComputeOps.kt:1435-1565). */
+private fun checkStatus(st: Int) {
+    if (st == LK_OK.toInt()) return
+    val msg = lk_last_error()?.toKString() ?: "lk_hip status $st"
+    when (st) {
+        LK_ERR_INVALID_ARG.toInt() -> throw IllegalArgumentException(msg)
+        LK_ERR_NOT_IMPLEMENTED.toInt() -> throw NotImplementedError(msg)
+        LK_ERR_OUT_OF_BOUNDS.toInt() -> throw IndexOutOfBoundsException(msg)
+        LK_ERR_NO_BUFFER.toInt() -> throw IllegalStateException(msg)
+        else -> throw IllegalStateException("HIP device error: $msg")
+    }
+}
+
+/** GGMLType -> lk_type: the ids of GGMLType.fromValue (K/core/GGMLTypes.kt:145-168). The enum's
+ *  ordinals differ from those ids past Q8_K (BITNET_1_58 sits at ordinal 14), so map by name. */
+private fun lkTypeId(t: GGMLType): Int = when (t) {
+    GGMLType.Q1_5_K -> LK_TYPE_Q1_5_K.toInt()
+    GGMLType.I8 -> LK_TYPE_I8.toInt()
+    GGMLType.I16 -> LK_TYPE_I16.toInt()
+    GGMLType.I32 -> LK_TYPE_I32.toInt()
+    GGMLType.I64 -> LK_TYPE_I64.toInt()
+    GGMLType.BITNET_1_58 -> LK_TYPE_BITNET_1_58.toInt()
+    else -> t.ordinal  // F32 .. Q8_K: ordinal == fromValue id
+}
+
+/** Fill an lk_tensor from a GGMLTensor whose bytes live in a pinned ByteArray. */
+private fun fill(t: lk_tensor, src: GGMLTensor, base: CPointer<ByteVar>?, bytes: Int) {
+    t.type = lkTypeId(src.type)
+    for (i in 0 until 4) {
+        t.ne[i] = src.ne[i]
+        t.nb[i] = src.nb[i]
+    }
+    t.data = base
+    t.buf_bytes = bytes.toULong()
+    t.data_offset = src.dataOffset
+}
+
+/**
+ * computeMatMul(graphAllocator, context, a, b, dst) on the MI355X: same signature, same
+ * destination-tensor semantics, same exceptions. Weights are mirrored on the device once per
+ * (ByteArray, offset, size, generation) by lk_weights_pin; activations and dst are copied per call.
+ */
+fun computeMatMulHip(graphAllocator: GGMLGraphAllocator, @Suppress("unused") context: GGMLContext,
+                     a: GGMLTensor, b: GGMLTensor, dst: GGMLTensor, weightGeneration: ULong = 0u) {
+    val bufA = graphAllocator.buffers.getOrNull(a.bufferId)
+    val bufB = graphAllocator.buffers.getOrNull(b.bufferId)
+    val bufD = graphAllocator.buffers.getOrNull(dst.bufferId)
+    memScoped {
+        val la = alloc<lk_tensor>()
+        val lb = alloc<lk_tensor>()
+        val ld = alloc<lk_tensor>()
+        // Pin the three ByteArrays for the duration of the call (the library copies what it needs).
+        (bufA ?: ByteArray(0)).usePinned { pa ->
+            (bufB ?: ByteArray(0)).usePinned { pb ->
+                (bufD ?: ByteArray(0)).usePinned { pd ->
+                    fill(la, a, if (bufA != null && bufA.isNotEmpty()) pa.addressOf(0) else null, bufA?.size ?: 0)
+                    fill(lb, b, if (bufB != null && bufB.isNotEmpty()) pb.addressOf(0) else null, bufB?.size ?: 0)
+                    fill(ld, dst, if (bufD != null && bufD.isNotEmpty()) pd.addressOf(0) else null, bufD?.size ?: 0)
+                    if (a.type == GGMLType.Q4_0 || a.type == GGMLType.Q4_1 || a.type == GGMLType.Q8_0) {
+                        checkStatus(lk_weights_pin(la.ptr, weightGeneration))
+                    }
+                    checkStatus(lk_mul_mat(la.ptr, lb.ptr, ld.ptr))
+                }
+            }
+        }
+    }
+}
+
+/** A GGMLBackend that offloads MUL_MAT to the MI355X and defers everything else to the CPU backend. */
+class GGMLHipBackend(private val device: Int = 0) : GGMLBackend {
+    private val cpu = GGMLCpuBackend()
+
+    init {
+        checkStatus(lk_init(device))
+    }
+
+    override fun getGuid(): String = "HIP-GFX950-LK"
+    override fun getName(): String = "HIP"
+    override fun free() = lk_shutdown()
+    override fun getDefaultBufferType(): GGMLBackendBufferType = cpu.getDefaultBufferType()  // host ByteArrays stay authoritative
+
+    override fun supportsOp(tensor: GGMLTensor): Boolean {
+        if (tensor.op != GGMLOp.MUL_MAT) return false
+        val a = tensor.src[0] ?: return false
+        val b = tensor.src[1] ?: return false
+        val quant = (a.type == GGMLType.Q4_0 || a.type == GGMLType.Q4_1 || a.type == GGMLType.Q8_0) &&
+            b.type == GGMLType.F32 && tensor.type == GGMLType.F32
+        val general = (a.type == GGMLType.F32 && b.type == GGMLType.F32 && tensor.type == GGMLType.F32) ||
+            (a.type == GGMLType.F16 && b.type == GGMLType.F16 && tensor.type == GGMLType.F16)
+        return quant || general
+    }
+
+    override fun supportsBufferType(bufferType: GGMLBackendBufferType): Boolean = bufferType.isHost()
+
+    override fun graphCompute(graph: GGMLCGraph): GGMLStatus {
+        val ga = graph.allocator ?: return GGMLStatus.FAILED
+        return try {
+            for (i in 0 until graph.nNodes) {
+                val node = graph.nodes[i] ?: continue
+                if (supportsOp(node)) {
+                    computeMatMulHip(ga, ga.context, node.src[0]!!, node.src[1]!!, node)
+                } else {
+                    // one-node graph on the CPU backend (K/core/GGMLCpuBackend.kt:167-176)
+                    val one = GGMLCGraph(size = 1, nNodes = 1, nodes = arrayOf(node), allocator = ga)
+                    if (cpu.graphCompute(one) != GGMLStatus.SUCCESS) return GGMLStatus.FAILED
+                }
+            }
+            GGMLStatus.SUCCESS
+        } catch (e: Exception) {
+            println("GGMLHipBackend: Error computing graph: ${e.message}")
+            GGMLStatus.FAILED
+        }
+    }
+}
