@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-headline", action="store_true")
     ap.add_argument("--no-chain", action="store_true")
+    ap.add_argument("--no-batched", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=6144)
     args = ap.parse_args()
@@ -233,6 +234,8 @@ def main():
         result["decode_chain"] = decode_chain(torch, G, ga, nodes_by_layer, compute, token_bytes)
     if rank == 0 and world == 1 and not args.no_headline:
         result["headline_q4_0_4096x4096_n1"] = headline(torch, G, dev)
+    if rank == 0 and world == 1 and not args.no_batched:
+        result["batched"] = batched(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, token_bytes)
     if rank == 0:
@@ -366,6 +369,56 @@ def headline(torch, G, dev, copies=48, reps=20):
             "rotating_weight_copies": copies,
             "grouped_48_in_one_launch": {"avg_launch_us": round(per_grouped * 1e6, 3), "achieved_GBps": round(gbs_g, 1),
                                          "frac_of_8TBps": round(gbs_g / HBM_PEAK_GBS, 4)}}
+
+
+def batched(torch, G, dev, reps=10):
+    """SURVEY §8d configs C3 (Q4_0 11008x4096, N = 32: HBM-bound) and C5 (Q4_0 4096x4096, N = 512:
+    MFMA-bound) through computeMatMul (xsplit_kernel + gemm_q_lds_kernel), one call per matrix,
+    rotating over distinct weight copies (> Infinity Cache), graph-replayed. Reports algorithmic
+    GB/s, useful TFLOP/s (2·M·N·K) and the MFMA-issued rate (2 bf16 MFMAs per useful one:
+    x = hi + lo)."""
+    T = G.GGMLType
+    out = {}
+    for name, M, K, N, copies in (("c3_q4_0_11008x4096_n32", 11008, 4096, 32, 16), ("c5_q4_0_4096x4096_n512", 4096, 4096, 512, 32)):
+        nb = M * K // 32 * Q4_0_BLOCK
+        g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+        wb = g.addBuffer(copies * nb + 256)
+        xb = g.addBuffer(4 * K * N + 256)
+        db = g.addBuffer(4 * M * N * copies + 256)
+        src = torch.randn(M * K, device=dev) * 0.02
+        for c in range(copies):
+            g.buffers[wb][c * nb:(c + 1) * nb].copy_(G.quantizeTensor(src * (1 + 0.01 * c), T.Q4_0))
+        g.buffers[xb][: 4 * K * N].copy_(torch.randn(K * N, device=dev).view(torch.uint8))
+        nodes = [(G.GGMLTensor(T.Q4_0, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [N, K], bufferId=xb),
+                  G.GGMLTensor(T.F32, [N, M], bufferId=db, dataOffset=4 * M * N * c)) for c in range(copies)]
+        s = torch.cuda.Stream(device=dev)
+
+        def run_all():
+            for (a, b, d) in nodes:
+                G.computeMatMul(g, None, a, b, d, stream=s)
+
+        with torch.cuda.stream(s):
+            run_all()
+        torch.cuda.synchronize()
+        gr = capture(torch, run_all, s)
+        fn = gr.replay if gr is not None else run_all
+        with torch.cuda.stream(s):
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
+                fn()
+            e1.record(s)
+        torch.cuda.synchronize()
+        per = e0.elapsed_time(e1) / 1e3 / (reps * copies)
+        nbytes = alg_bytes(M, K, N)
+        tf = 2 * M * N * K / per / 1e12
+        out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
+                     "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "useful_TFLOPs": round(tf, 2),
+                     "mfma_issued_TFLOPs": round(2 * tf, 2), "frac_of_2500TF_bf16": round(2 * tf / 2500, 4),
+                     "rotating_weight_copies": copies, "hip_graph": gr is not None}
+        del g
+    return out
 
 
 def cpu_baseline(sample_rows, token_bytes):

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -282,7 +283,171 @@ int launch_gemv_v1(int32_t qt, const GemvDesc &d, hipStream_t st) {
   return LK_OK;
 }
 
-int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+// Batched quantized GEMM on MFMA: N >= 2, whole blocks per row (K % 32 == 0).
+bool gemm_eligible(const Checked &c) {
+  return c.path == Path::kQuantF32 && c.N >= 2 && c.K > 0 && (c.K % 32) == 0 && c.M <= INT32_MAX &&
+         c.N <= INT32_MAX && c.K <= INT32_MAX;
+}
+
+// Device scratch for the GEMM (activation fragments, block sums, split-K partials, tile
+// counters), per device, grow-only. Allocated outside any capture on first use; counters are
+// zeroed once and re-armed by the kernel.
+struct GemmScratch {
+  void *frag = nullptr; size_t frag_bytes = 0;
+  void *partial = nullptr; size_t partial_bytes = 0;
+  int32_t *counter = nullptr; size_t counter_n = 0;
+};
+GemmScratch &gemm_scratch() {
+  static GemmScratch per_dev[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  return per_dev[dev];
+}
+int grow(void **p, size_t *have, size_t want) {
+  if (*have >= want) return LK_OK;
+  if (*p) HIP_TRY(hipFree(*p));
+  *p = nullptr;
+  *have = 0;
+  HIP_TRY(hipMalloc(p, want));
+  *have = want;
+  return LK_OK;
+}
+
+int gemm_occupancy() {  // LK_GEMM_OCC overrides (tuning only)
+  static int occ = [] {
+    const char *e = getenv("LK_GEMM_OCC");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 4;
+  }();
+  return occ;
+}
+
+template <int QT, int WM, int WN, int MT, int NT>
+int launch_gemm_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
+  constexpr int BM = WM * MT * 16, BN = WN * NT * 16;
+  GemmScratch &S = gemm_scratch();
+  g.tiles_m = (g.M + BM - 1) / BM;
+  g.tiles_n = (g.N + BN - 1) / BN;
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int nblk = g.K / 32;
+  // split K until the grid holds ~gemm_occupancy() workgroups per CU (latency hiding)
+  int slices = std::max(1, std::min({(gemm_occupancy() * cu_count() + tiles - 1) / tiles, 32, nblk}));
+  g.kslice = (nblk + slices - 1) / slices;
+  slices = (nblk + g.kslice - 1) / g.kslice;
+  g.slices = slices;
+  if (slices > 1) {
+    int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * tiles * BM * BN * sizeof(float));
+    if (rc) return rc;
+    if (S.counter_n < (size_t)tiles) {
+      void *c = S.counter;
+      size_t cb = S.counter_n * sizeof(int32_t);
+      rc = grow(&c, &cb, (size_t)tiles * sizeof(int32_t));
+      if (rc) return rc;
+      S.counter = (int32_t *)c;
+      S.counter_n = (size_t)tiles;
+      HIP_TRY(hipMemset(S.counter, 0, S.counter_n * sizeof(int32_t)));
+    }
+    g.partial = (float *)S.partial;
+    g.counter = S.counter;
+  }
+  const int64_t ntx = (g.N + 15) / 16;
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  hipLaunchKernelGGL((gemm_q_mfma_kernel<QT, WM, WN, MT, NT>), dim3((unsigned)(tiles * slices)), dim3(256), 0, st, g);
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+// LDS-DMA pipelined GEMM (gemm_q_lds_kernel): K % 128 == 0 and weight rows aligned for its
+// DMA pieces. One workgroup (4 waves, ~100-150 KB of LDS) per CU; split K to fill the grid.
+bool gemm_lds_eligible(int32_t qt, const lk_tensor *a, const Checked &c) {
+  if ((c.K / 32) % kLdsSB) return false;
+  const uintptr_t base = (uintptr_t)a->data + a->data_offset;
+  if (base % 8) return false;  // rows start 8-byte aligned for the 16-byte DMA pieces
+  // the last row's last stage reads up to OVERREAD bytes past the matrix: they must be in the buffer
+  const uint64_t over = qt == LK_TYPE_Q4_0 ? LdsGemmGeom<LK_TYPE_Q4_0, 2>::OVERREAD
+                       : qt == LK_TYPE_Q4_1 ? LdsGemmGeom<LK_TYPE_Q4_1, 2>::OVERREAD
+                                            : LdsGemmGeom<LK_TYPE_Q8_0, 2>::OVERREAD;
+  return c.a_hi + over <= a->buf_bytes;
+}
+
+template <int QT, int NT>
+int launch_gemm_lds_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
+  using GG = LdsGemmGeom<QT, NT>;
+  GemmScratch &S = gemm_scratch();
+  g.tiles_m = (g.M + GG::BM - 1) / GG::BM;
+  g.tiles_n = (g.N + GG::BN - 1) / GG::BN;
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int nst = g.K / 32 / GG::SB;  // stages over the whole K
+  int slices = std::max(1, std::min({(gemm_occupancy() * cu_count() / 4 + tiles - 1) / tiles, 32, nst}));
+  g.kslice = ((nst + slices - 1) / slices) * GG::SB;
+  slices = (g.K / 32 + g.kslice - 1) / g.kslice;
+  g.slices = slices;
+  if (slices > 1) {
+    int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * tiles * GG::BM * GG::BN * sizeof(float));
+    if (rc) return rc;
+    if (S.counter_n < (size_t)tiles) {
+      void *c = S.counter;
+      size_t cb = S.counter_n * sizeof(int32_t);
+      rc = grow(&c, &cb, (size_t)tiles * sizeof(int32_t));
+      if (rc) return rc;
+      S.counter = (int32_t *)c;
+      S.counter_n = (size_t)tiles;
+      HIP_TRY(hipMemset(S.counter, 0, S.counter_n * sizeof(int32_t)));
+    }
+    g.partial = (float *)S.partial;
+    g.counter = S.counter;
+  }
+  const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  constexpr size_t lds = GG::LDS;
+  hipLaunchKernelGGL((gemm_q_lds_kernel<QT, NT>), dim3((unsigned)(tiles * slices)), dim3(256), lds, st, g);
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+template <int QT>
+int launch_gemm_qt(const GemmArgs &g, const XSplitArgs &xa, bool lds_ok, hipStream_t st) {
+  if (lds_ok) {
+    if (g.N <= 16) return launch_gemm_lds_t<QT, 1>(g, xa, st);
+    if (g.N <= 32) return launch_gemm_lds_t<QT, 2>(g, xa, st);
+    return launch_gemm_lds_t<QT, 4>(g, xa, st);
+  }
+  if (g.N <= 16) return launch_gemm_t<QT, 4, 1, 2, 1>(g, xa, st);
+  if (g.N <= 32) return launch_gemm_t<QT, 4, 1, 2, 2>(g, xa, st);
+  return launch_gemm_t<QT, 2, 2, 2, 2>(g, xa, st);
+}
+
+int launch_gemm(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  GemmScratch &S = gemm_scratch();
+  const int64_t nblk = c.K / 32, ntx = (c.N + 15) / 16;
+  const size_t fb = (size_t)ntx * nblk * kXSplits * 64 * 16, sb = (size_t)nblk * ntx * 16 * sizeof(float);
+  int rc = grow(&S.frag, &S.frag_bytes, fb + sb);
+  if (rc) return rc;
+  XSplitArgs xa{};
+  xa.b = (const uint8_t *)b->data + b->data_offset;
+  xa.b_nb0 = b->nb[0]; xa.b_nb1 = b->nb[1];
+  xa.N = c.N; xa.K = c.K;
+  xa.frag = (u32x4 *)S.frag;
+  xa.xsum = (float *)((uint8_t *)S.frag + fb);
+  xa.mult = a->type == LK_TYPE_Q4_0 ? GemmQ<LK_TYPE_Q4_0>::MULT : 1.f;
+  xa.q4_order = a->type != LK_TYPE_Q8_0;
+  const bool lds_ok = gemm_lds_eligible(a->type, a, c);
+  GemmArgs g{};
+  g.a = (const uint8_t *)a->data + a->data_offset;
+  g.frag = xa.frag;
+  g.xsum = xa.xsum;
+  g.dst = (uint8_t *)dst->data + dst->data_offset;
+  g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
+  g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
+  switch (a->type) {
+    case LK_TYPE_Q4_0: return launch_gemm_qt<LK_TYPE_Q4_0>(g, xa, lds_ok, st);
+    case LK_TYPE_Q4_1: return launch_gemm_qt<LK_TYPE_Q4_1>(g, xa, lds_ok, st);
+    case LK_TYPE_Q8_0: return launch_gemm_qt<LK_TYPE_Q8_0>(g, xa, lds_ok, st);
+    default: return fail(LK_ERR_NOT_IMPLEMENTED, "gemm: type %d", a->type);
+  }
+}
+
+GenericArgs make_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c) {
   GenericArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
   g.b = (const uint8_t *)b->data + b->data_offset;
@@ -291,6 +456,11 @@ int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const
   g.a_nb0 = a->nb[0]; g.a_nb1 = a->nb[1];
   g.b_nb0 = b->nb[0]; g.b_nb1 = b->nb[1];
   g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
+  return g;
+}
+
+int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  const GenericArgs g = make_generic(a, b, dst, c);
   const int64_t waves = c.M * c.N;
   const int64_t blocks = (waves + 3) / 4;
   if (blocks > (int64_t)INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "output too large for the generic kernel");
@@ -327,6 +497,7 @@ int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *ds
     return launch_generic(a, b, dst, c, st);
   }
   if (gemv_eligible(a, b, dst, c)) return run_single_gemv(a, b, dst, c, st);
+  if (gemm_eligible(c)) return launch_gemm(a, b, dst, c, st);
   return launch_generic(a, b, dst, c, st);
 }
 

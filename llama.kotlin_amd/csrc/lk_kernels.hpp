@@ -571,13 +571,459 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
   LK_TRACE(3);
 }
 
-// ---- generic path (any K, any byte strides, ragged blocks) ----------------------
-
 struct GenericArgs {
   const uint8_t *a; const uint8_t *b; uint8_t *dst; // buffer base + dataOffset
   int64_t M, N, K;
   int64_t a_nb0, a_nb1, b_nb0, b_nb1, d_nb0, d_nb1; // byte strides (A's used for F32/F16 only)
 };
+
+// ---- batched (N > 1) quantized GEMM on MFMA ------------------------------------
+//
+// dst(n, m) = Σ_blocks d_blk(m) · (Σ_k c_k(m) · x(n, k)) on v_mfma_f32_16x16x32_bf16, computed
+// transposed (C'[n][m] = X[n][k] · W[k][m]) so that a lane's weight row m is also its output
+// column: the lane that reads row m's codes applies row m's block scale, and 4 consecutive n of
+// one row leave as one 16-byte store. One MFMA spans exactly one 32-weight block.
+//
+// Weight operand (exact in bf16; small magnitudes: the bf16 MFMA's sum is only ~2⁻¹⁷-accurate
+// relative to its largest terms, so the codes stay centred or small):
+//   Q4_0: n·2⁻⁹ (fp8 conversion of the masked nibble); the −8 offset enters through the MFMA's
+//         C input, C = T = −2⁻⁶·Σx per (block, column) from xsplit_kernel, so p = 2⁻⁹·Σ(n−8)·x;
+//         scale 512·d.
+//   Q4_1: n·2⁻⁹, scale 512·d, plus m·Σx per block (T = Σx, applied in f32 after the MFMA).
+//   Q8_0: q (int8 -> f32 -> bf16), scale d.
+// Within a lane's 8 codes the k order is (0,2,4,6,1,3,5,7) for the Q4 types (the order the
+// fp8 conversions of the masked nibbles yield); xsplit_kernel writes the activations in it.
+//
+// Activations: x = hi + lo, hi = bf16(x) truncated, lo = bf16(x − hi) rounded to nearest:
+// |x − (hi + lo)| ≤ 2⁻¹⁷|x| at any f32 exponent. Products are exact, sums are f32; the outputs
+// are within 2⁻¹⁷·Σ|c·x| (+ f32 accumulation) of the exact product (tests/_util.py SPLIT_REL).
+//
+// xsplit_kernel writes operand fragments: x-tile t (16 columns), block kb, split s: lane l holds
+// x(n = 16t + (l&15), k = 32kb + 8(l>>4) + order[j]) at frag[((t·nblk + kb)·2 + s)·64 + l]
+// (16 B), so each operand is one contiguous 1-KB piece; T = mult·Σx at xsum[kb·N16 + n].
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kXSplits = 2;
+
+struct XSplitArgs {
+  const uint8_t *b;   // B(n, k) at n·nb0 + k·nb1
+  int64_t b_nb0, b_nb1;
+  int64_t N, K;
+  u32x4 *frag;        // [ntx][nblk][kXSplits][64] x 16 B
+  float *xsum;        // [nblk][N16]: mult · Σ_block x
+  float mult;
+  int32_t q4_order;   // 1: k order (0,2,4,6,1,3,5,7) within each 8
+};
+
+// One wave per (x-tile, block).
+__global__ __launch_bounds__(256) void xsplit_kernel(XSplitArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nblk = g.K / 32, ntx = (g.N + 15) / 16;
+  const int64_t idx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (idx >= ntx * nblk) return;
+  const int64_t t = idx / nblk, kb = idx % nblk;
+  const int64_t n = 16 * t + (lane & 15);
+  const int64_t k0 = 32 * kb + 8 * (lane >> 4);
+  float v[8];
+  float part = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int kk = g.q4_order ? ((j & 3) * 2 + (j >> 2)) : j;
+    v[j] = (n < g.N) ? *(const float *)(g.b + n * g.b_nb0 + (k0 + kk) * g.b_nb1) : 0.f;
+    part += v[j];
+  }
+  uint32_t hi[4], lo[4];
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    uint32_t h[2], l[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint32_t bx = __builtin_bit_cast(uint32_t, v[j + q]);
+      const float r = v[j + q] - __builtin_bit_cast(float, bx & 0xFFFF0000u);  // exact
+      uint32_t br = __builtin_bit_cast(uint32_t, r);
+      br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even (r is finite, |r| < 2^-7·|x|)
+      h[q] = bx;
+      l[q] = br;
+    }
+    hi[j / 2] = __builtin_amdgcn_perm(h[1], h[0], 0x07060302u);
+    lo[j / 2] = __builtin_amdgcn_perm(l[1], l[0], 0x07060302u);
+  }
+  g.frag[(idx * kXSplits + 0) * 64 + lane] = u32x4{hi[0], hi[1], hi[2], hi[3]};
+  g.frag[(idx * kXSplits + 1) * 64 + lane] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+  part += __shfl_xor(part, 16, kWave);
+  part += __shfl_xor(part, 32, kWave);
+  if (lane < 16) g.xsum[kb * (ntx * 16) + n] = g.mult * part;
+}
+
+// two f32 whose values fit in 8 significant bits -> their exact bf16 pair (lo, hi)
+__device__ __forceinline__ uint32_t pack_bf16_exact(float lo, float hi) {
+  return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07060302u);
+}
+
+// Weight operand of one block for the lane's row, from the code dword(s) of lane group g.
+template <int QT> __device__ __forceinline__ bf16x8 w_frag(uint32_t u0, uint32_t u1);
+template <int QT> struct Q4Frag {
+  static __device__ __forceinline__ bf16x8 make(uint32_t u) {
+    const uint32_t lo = u & 0x0F0F0F0Fu, hi = (u >> 4) & 0x0F0F0F0Fu;  // n0,n2,n4,n6 / n1,n3,n5,n7
+    const f2v e0 = fp8x2<false>(lo), e1 = fp8x2<true>(lo), o0 = fp8x2<false>(hi), o1 = fp8x2<true>(hi);
+    uint32_t w[4] = {pack_bf16_exact(e0.x, e0.y), pack_bf16_exact(e1.x, e1.y), pack_bf16_exact(o0.x, o0.y),
+                     pack_bf16_exact(o1.x, o1.y)};
+    return __builtin_bit_cast(bf16x8, w);  // n·2⁻⁹ for k = 0,2,4,6,1,3,5,7
+  }
+};
+template <> __device__ __forceinline__ bf16x8 w_frag<LK_TYPE_Q4_0>(uint32_t u, uint32_t) { return Q4Frag<0>::make(u); }
+template <> __device__ __forceinline__ bf16x8 w_frag<LK_TYPE_Q4_1>(uint32_t u, uint32_t) { return Q4Frag<0>::make(u); }
+template <>
+__device__ __forceinline__ bf16x8 w_frag<LK_TYPE_Q8_0>(uint32_t u0, uint32_t u1) {
+  u0 ^= 0x80808080u;
+  u1 ^= 0x80808080u;
+  const f2v off = {-128.f, -128.f};
+  const f2v a = f2v{(float)(u0 & 0xFF), (float)((u0 >> 8) & 0xFF)} + off, b = f2v{(float)((u0 >> 16) & 0xFF), (float)(u0 >> 24)} + off,
+            c = f2v{(float)(u1 & 0xFF), (float)((u1 >> 8) & 0xFF)} + off, d = f2v{(float)((u1 >> 16) & 0xFF), (float)(u1 >> 24)} + off;
+  uint32_t w[4] = {pack_bf16_exact(a.x, a.y), pack_bf16_exact(b.x, b.y), pack_bf16_exact(c.x, c.y), pack_bf16_exact(d.x, d.y)};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+template <int QT> struct GemmQ {
+  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr bool USES_T = (QT != LK_TYPE_Q8_0);  // per-(block, column) sums needed
+  static constexpr bool C_FROM_T = (QT == LK_TYPE_Q4_0);  // T is the MFMA's C input
+  static constexpr bool HAS_MIN = (QT == LK_TYPE_Q4_1);  // acc += s2·T after the MFMA
+  static constexpr float MULT = (QT == LK_TYPE_Q4_0) ? -0.015625f : 1.f;  // T = MULT·Σx
+  static constexpr int CODE = (QT == LK_TYPE_Q4_1) ? 4 : 2;  // byte offset of the codes in a block
+  static constexpr int GSTRIDE = (QT == LK_TYPE_Q8_0) ? 8 : 4;
+};
+
+// Code dword(s) of lane group g and the block scale terms: acc += s1·p (+ s2·T for Q4_1).
+template <int QT, typename Ptr>
+__device__ __forceinline__ void read_block(Ptr blk, int g, uint32_t &u0, uint32_t &u1, float &s1, float &s2) {
+  typedef uint16_t u16_ua __attribute__((aligned(1)));
+  typedef uint32_t u32_ua __attribute__((aligned(1)));
+  const float d = h2f(*(const u16_ua *)blk);
+  s1 = (QT == LK_TYPE_Q8_0) ? d : 512.f * d;
+  u0 = *(const u32_ua *)(blk + GemmQ<QT>::CODE + GemmQ<QT>::GSTRIDE * g);
+  u1 = (QT == LK_TYPE_Q8_0) ? *(const u32_ua *)(blk + 6 + 8 * g) : 0u;
+  s2 = GemmQ<QT>::HAS_MIN ? h2f(*(const u16_ua *)(blk + 2)) : 0.f;  // m
+}
+
+struct GemmArgs {
+  const uint8_t *a;      // weights (buffer base + dataOffset)
+  const u32x4 *frag;     // xsplit output
+  const float *xsum;
+  uint8_t *dst;
+  int64_t d_nb0, d_nb1;
+  int32_t M, N, K;
+  int32_t tiles_m, tiles_n, slices, kslice;  // split-K: slice s covers blocks [s·kslice, (s+1)·kslice)
+  float *partial;        // [slices][tiles_m·tiles_n][BM·BN] (slices > 1)
+  int32_t *counter;      // [tiles_m·tiles_n], zero between launches
+};
+
+// acc += s1·p (+ s2·T for Q4_1), as packed FMAs.
+template <bool HAS_MIN>
+__device__ __forceinline__ void accumulate(f32x4 &acc, float s1, float s2, f32x4 p, f32x4 t) {
+  f2v a0 = {acc.x, acc.y}, a1 = {acc.z, acc.w};
+  if constexpr (HAS_MIN) {
+    const f2v m2 = {s2, s2};
+    a0 = __builtin_elementwise_fma(m2, f2v{t.x, t.y}, a0);
+    a1 = __builtin_elementwise_fma(m2, f2v{t.z, t.w}, a1);
+  }
+  const f2v m1 = {s1, s1};
+  a0 = __builtin_elementwise_fma(m1, f2v{p.x, p.y}, a0);
+  a1 = __builtin_elementwise_fma(m1, f2v{p.z, p.w}, a1);
+  acc = f32x4{a0.x, a0.y, a1.x, a1.y};
+}
+
+// Epilogue shared by the GEMM kernels: lane holds C'(n = 16·xtile + 4(lane>>4) + e, m = row),
+// e = 0..3. slices == 1: store. Split-K: publish this slice's tile; the last slice to arrive sums
+// all slices in slice order (deterministic) and stores, then re-arms the tile counter.
+template <int MT, int NT, int BM, int BN>
+__device__ __forceinline__ void gemm_finish(const GemmArgs &g, f32x4 (&acc)[MT][NT], int tile, int tiles, int slice, int tm,
+                                            int tn, int wm, int wn, int wave, int lane) {
+  const int gq = lane >> 4;
+  auto store = [&](int i, int j, f32x4 v) __attribute__((always_inline)) {
+    const int64_t m = (int64_t)tm * BM + (wm * MT + i) * 16 + (lane & 15);
+    const int64_t n0 = (int64_t)(tn * (BN / 16) + wn * NT + j) * 16 + gq * 4;
+    if (m >= g.M) return;
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    if (g.d_nb0 == 4 && n0 + 4 <= g.N && ((((uintptr_t)g.dst + m * g.d_nb1 + n0 * 4) & 15) == 0)) {
+      *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = v;
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e[q];
+  };
+  if (g.slices == 1) {
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+      for (int j = 0; j < NT; j++) store(i, j, acc[i][j]);
+    return;
+  }
+  const int tile_elems = BM * BN;
+  const int lin0 = wave * MT * NT * 256;  // wave-local layout: [wave][i][j][lane][4]
+  float *mine = g.partial + ((int64_t)slice * tiles + tile) * tile_elems;
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) ((f32x4 *)mine)[(lin0 + (i * NT + j) * 256) / 4 + lane] = acc[i][j];
+  __threadfence();
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0) last = (atomicAdd(&g.counter[tile], 1) == g.slices - 1);
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl < g.slices; sl++) {
+        const f32x4 v = __builtin_nontemporal_load(
+            (const f32x4 *)(g.partial + ((int64_t)sl * tiles + tile) * tile_elems) + (lin0 + (i * NT + j) * 256) / 4 + lane);
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+      }
+      store(i, j, sum);
+    }
+  if (threadIdx.x == 0) g.counter[tile] = 0;
+}
+
+// Direct-load variant (any K % 32 == 0): 4 waves in a WM × WN grid, wave tile MT weight tiles
+// (16 rows) × NT x-tiles (16 columns); weights and activation fragments go global -> VGPRs one
+// block ahead of the MFMAs.
+template <int QT, int WM, int WN, int MT, int NT>
+__global__ __launch_bounds__(256) void gemm_q_mfma_kernel(GemmArgs g) {
+  using Q = GemmQ<QT>;
+  constexpr int BB = Q::BB;
+  constexpr int BM = WM * MT * 16, BN = WN * NT * 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int tile = (int)blockIdx.x % tiles, slice = (int)blockIdx.x / tiles;
+  const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
+  const int nblk = g.K / 32;
+  const int kb0 = slice * g.kslice, kb1 = min(kb0 + g.kslice, nblk);
+  const int64_t RB = (int64_t)nblk * BB;
+  const int gq = lane >> 4;
+  const int ntx = (g.N + 15) / 16;
+
+  int64_t wrow[MT];  // this lane's weight row per tile (clamped to M-1)
+#pragma unroll
+  for (int i = 0; i < MT; i++) wrow[i] = min((int64_t)tm * BM + (wm * MT + i) * 16 + (lane & 15), (int64_t)g.M - 1);
+  int xt[NT];        // x-tile index per tile (clamped)
+#pragma unroll
+  for (int j = 0; j < NT; j++) xt[j] = min(tn * (BN / 16) + wn * NT + j, ntx - 1);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const LK_GLOBAL u32x4 *fr = (const LK_GLOBAL u32x4 *)g.frag;
+  const LK_GLOBAL f32x4 *xs = (const LK_GLOBAL f32x4 *)g.xsum;
+  struct Blk {
+    uint32_t u0[MT], u1[MT];
+    float s1[MT], s2[MT];
+    u32x4 xf[NT][kXSplits];
+    f32x4 t[NT];
+  };
+  auto load_block = [&](int kb, Blk &o) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+      read_block<QT>((const LK_GLOBAL uint8_t *)g.a + wrow[i] * RB + (int64_t)kb * BB, gq, o.u0[i], o.u1[i], o.s1[i], o.s2[i]);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+#pragma unroll
+      for (int sp = 0; sp < kXSplits; sp++) o.xf[j][sp] = fr[(((int64_t)xt[j] * nblk + kb) * kXSplits + sp) * 64 + lane];
+      if constexpr (Q::USES_T) o.t[j] = xs[((int64_t)kb * (ntx * 16) + xt[j] * 16 + gq * 4) / 4];
+      else o.t[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  Blk cur, nxt;
+  if (kb0 < kb1) load_block(kb0, cur);
+  for (int kb = kb0; kb < kb1; kb++) {
+    if (kb + 1 < kb1) load_block(kb + 1, nxt);
+#pragma unroll
+    for (int i = 0; i < MT; i++) {
+      const bf16x8 wf = w_frag<QT>(cur.u0[i], cur.u1[i]);
+#pragma unroll
+      for (int j = 0; j < NT; j++) {
+        f32x4 p = Q::C_FROM_T ? cur.t[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+        p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur.xf[j][1]), wf, p, 0, 0, 0);
+        p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur.xf[j][0]), wf, p, 0, 0, 0);
+        accumulate<Q::HAS_MIN>(acc[i][j], cur.s1[i], cur.s2[i], p, cur.t[j]);
+      }
+    }
+    if (kb + 1 < kb1) cur = nxt;
+  }
+  gemm_finish<MT, NT, BM, BN>(g, acc, tile, tiles, slice, tm, tn, wm, wn, wave, lane);
+}
+
+// LDS-DMA issued through inline asm: the compiler's waitcnt pass cannot tell which LDS bytes a
+// pending global_load_lds writes and inserts vmcnt(0) before LDS reads it cannot disambiguate,
+// which drains the whole ring every stage. Hidden from it, the kernel orders the DMA itself
+// (counted vmcnt + s_barrier). SGPR base + 32-bit VGPR offset; M0 = wave-uniform LDS
+// destination, lane i lands at M0 + 16i. (Only 16-byte pieces: a 12-byte piece does not land
+// at M0 + 12i.)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+template <bool NT>
+__device__ __forceinline__ void dma16(const void *sbase, uint32_t vofs, const void *lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LK_LDS const void *)lds_dst);
+  if constexpr (NT) asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
+  else asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// LDS-DMA pipelined variant: 4 waves stacked along M (wave tile: MT = 2 weight tiles × NT
+// x-tiles; BM = 128, BN = 16·NT), K in stages of SB = 4 blocks. Each stage — the workgroup's
+// 128 rows × 4 blocks of raw weight bytes (rounded up to 16-byte pieces; rows then start
+// 8-byte aligned), the 4·NT·2 activation fragments (1 KB each) and the T sums — moves
+// global -> LDS by LDS-DMA into a ring of D stages. Every wave issues the same number of DMA
+// instructions per stage, so a counted vmcnt plus one barrier publishes a stage, and D-1 stages
+// stay in flight while the MFMAs consume the oldest. Per-lane DMA offsets are fixed for the
+// launch; only the SGPR bases move with the stage.
+constexpr int kLdsSB = 4;
+
+template <int QT, int NT> struct LdsGemmGeom {
+  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr int SB = kLdsSB;
+  static constexpr int MT = 2, BM = 128, BN = 16 * NT;
+  static constexpr int AROWP = (SB * BB + 15) / 16 * 16;   // LDS bytes per row per stage
+  static constexpr int A_INST = BM * (AROWP / 16) / 64;     // DMA instructions for A
+  static constexpr int X_INST = SB * NT * kXSplits;
+  static constexpr int T_INST = GemmQ<QT>::USES_T ? 1 : 0;
+  static constexpr int NINST = A_INST + X_INST + T_INST;
+  static constexpr int C = (NINST + 3) / 4;                 // per wave per stage (padded)
+  static constexpr int A_BYTES = BM * AROWP;
+  static constexpr int X_BYTES = X_INST * 1024;
+  static constexpr int T_BYTES = T_INST * 1024;
+  static constexpr int STAGE = A_BYTES + X_BYTES + T_BYTES;
+  static constexpr int DFIT = (150 * 1024) / STAGE;
+  static constexpr int D = DFIT > 4 ? 4 : DFIT;
+  static constexpr int LDS = D * STAGE;
+  static constexpr int OVERREAD = AROWP - SB * BB;          // bytes read past a row's stage bytes
+  static_assert((BM * (AROWP / 16)) % 64 == 0, "A pieces");
+  static_assert(SB * BN / 4 <= 64, "T sums in one DMA instruction");
+  static_assert(D >= 2, "ring");
+  static_assert((D - 1) * C < 64, "vmcnt");
+};
+
+template <int QT, int NT>
+__global__ __launch_bounds__(256) void gemm_q_lds_kernel(GemmArgs g) {
+  using G = LdsGemmGeom<QT, NT>;
+  using Q = GemmQ<QT>;
+  constexpr int MT = G::MT, BM = G::BM, BN = G::BN, BB = G::BB, SB = G::SB;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int tile = (int)blockIdx.x % tiles, slice = (int)blockIdx.x / tiles;
+  const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
+  const int nblk = g.K / 32;
+  const int kb0 = slice * g.kslice, kb1 = min(kb0 + g.kslice, nblk);
+  const int nst = (kb1 - kb0) / SB;  // stages (kslice is a multiple of SB)
+  const int64_t RB = (int64_t)nblk * BB;
+  const int gq = lane >> 4;
+  const int ntx = (g.N + 15) / 16;
+  const int n16 = ntx * 16;
+
+  // This wave's DMA instructions q = wave·C + c (padding repeats the last): kind (0 A, 1 X, 2 T),
+  // per-lane byte offset from the kind's stage base, and LDS byte offset within a stage.
+  uint32_t vofs[G::C];
+  int kind[G::C], ldso[G::C];
+#pragma unroll
+  for (int c = 0; c < G::C; c++) {
+    const int q = min(wave * G::C + c, G::NINST - 1);
+    if (q < G::A_INST) {
+      const int piece = q * 64 + lane;
+      const int r = piece / (G::AROWP / 16), pc = piece % (G::AROWP / 16);
+      const int64_t row = min((int64_t)tm * BM + r, (int64_t)g.M - 1);
+      kind[c] = 0; vofs[c] = (uint32_t)(row * RB + pc * 16); ldso[c] = q * 1024;
+    } else if (q < G::A_INST + G::X_INST) {
+      const int x = q - G::A_INST;  // (block b, tile j, split sp)
+      const int b = x / (NT * kXSplits), j = (x / kXSplits) % NT, sp = x % kXSplits;
+      const int xt = min(tn * NT + j, ntx - 1);
+      kind[c] = 1; vofs[c] = (uint32_t)((((int64_t)xt * nblk + b) * kXSplits + sp) * 1024 + lane * 16);
+      ldso[c] = G::A_BYTES + x * 1024;
+    } else {
+      const int li = min(lane, SB * BN / 4 - 1);  // lane -> (block li / (BN/4), 4 columns)
+      const int b = li / (BN / 4), c4 = li % (BN / 4);
+      const int n = min(tn * BN + 4 * c4, n16 - 4);
+      kind[c] = 2; vofs[c] = (uint32_t)(((int64_t)b * n16 + n) * 4); ldso[c] = G::A_BYTES + G::X_BYTES;
+    }
+  }
+  auto issue_stage = [&](int st, int sl) __attribute__((always_inline)) {
+    const int kb = kb0 + min(st, nst - 1) * SB;  // past the last stage: reload the last (never read)
+    const uint8_t *base_a = g.a + (int64_t)kb * BB;
+    const uint8_t *base_x = (const uint8_t *)g.frag + (int64_t)kb * kXSplits * 1024;
+    const uint8_t *base_t = (const uint8_t *)(g.xsum + (int64_t)kb * n16);
+    uint8_t *slot = smem + sl * G::STAGE;
+#pragma unroll
+    for (int c = 0; c < G::C; c++) {
+      const uint8_t *base = kind[c] == 0 ? base_a : kind[c] == 1 ? base_x : base_t;
+      if (kind[c] == 0) dma16<LK_WEIGHT_AUX == 2>(base, vofs[c], slot + ldso[c]);
+      else dma16<false>(base, vofs[c], slot + ldso[c]);
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nst > 0) {
+    for (int st = 0; st < G::D; st++) issue_stage(st, st);
+    int slot = 0;
+    for (int st = 0; st < nst; st++) {
+      wait_vmcnt<(G::D - 1) * G::C>();
+      __builtin_amdgcn_s_barrier();
+      const uint8_t *A = smem + slot * G::STAGE;
+      const uint8_t *X = A + G::A_BYTES;
+      const float *T = (const float *)(X + G::X_BYTES);
+#pragma unroll
+      for (int b = 0; b < SB; b++) {
+        bf16x8 wf[MT];
+        float s1[MT], s2[MT];
+#pragma unroll
+        for (int i = 0; i < MT; i++) {
+          const uint8_t *blk = A + ((wave * MT + i) * 16 + (lane & 15)) * G::AROWP + b * BB;
+          uint32_t u0, u1;
+          read_block<QT>(blk, gq, u0, u1, s1[i], s2[i]);
+          wf[i] = w_frag<QT>(u0, u1);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+          const u32x4 *xf = (const u32x4 *)(X + ((b * NT + j) * kXSplits) * 1024) + lane;
+          const bf16x8 xh = __builtin_bit_cast(bf16x8, xf[0]), xl = __builtin_bit_cast(bf16x8, xf[64]);
+          f32x4 t = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (Q::USES_T) t = *(const f32x4 *)(T + b * BN + j * 16 + gq * 4);
+#pragma unroll
+          for (int i = 0; i < MT; i++) {
+            f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl, wf[i], Q::C_FROM_T ? t : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, wf[i], p, 0, 0, 0);
+            accumulate<Q::HAS_MIN>(acc[i][j], s1[i], s2[i], p, t);
+          }
+        }
+      }
+      wait_lgkmcnt0();
+      __builtin_amdgcn_s_barrier();  // every wave is done with this slot
+      issue_stage(st + G::D, slot);
+      slot = (slot + 1 == G::D) ? 0 : slot + 1;
+    }
+    wait_vmcnt<0>();  // drain the padding stages before the workgroup's LDS is released
+  }
+  gemm_finish<MT, NT, BM, BN>(g, acc, tile, tiles, slice, tm, tn, wave, 0, wave, lane);
+}
+
+// ---- generic path (any K, any byte strides, ragged blocks) ----------------------
+
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
 __device__ __forceinline__ uint32_t ld_u16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }

@@ -8,7 +8,24 @@ import numpy as np
 REL_TOL = 1e-3
 
 
-def parity_ok(g: np.ndarray, r: np.ndarray, rel: float = REL_TOL) -> tuple[bool, str]:
+# The batched (N > 1) MFMA path splits each activation as x = hi + lo in bf16, which represents
+# x to within 2^-17·|x| (llama.kotlin_amd/csrc/lk_kernels.hpp, xsplit_kernel); products and
+# sums are exact / f32, so its outputs are within 2^-17·Σ_k |w_ik|·|x_kj| of the exact product.
+SPLIT_REL = 2.0 ** -17
+
+
+def acc_noise(w_abs: np.ndarray, x_abs: np.ndarray, split: bool = False) -> np.ndarray:
+    """Per-element allowance for the f32 accumulation noise of the reference's own sequential
+    sum (and ours): 4·sqrt(K)·2^-24·Σ_k |w_ik|·|x_kj|. The reference (oracle) itself deviates
+    from the exact product by up to ~3.6e-6·||r||_inf at K = 11008 (measured), which exceeds
+    the fixed 1e-6·||r||_inf floor below on small outputs. split=True adds the bound of the
+    batched path's activation split (SPLIT_REL·Σ|w||x|)."""
+    K = w_abs.shape[1]
+    s = w_abs.astype(np.float64) @ x_abs.astype(np.float64)
+    return (4.0 * np.sqrt(K) * 2.0 ** -24 + (SPLIT_REL if split else 0.0)) * s
+
+
+def parity_ok(g: np.ndarray, r: np.ndarray, rel: float = REL_TOL, noise: np.ndarray | None = None) -> tuple[bool, str]:
     g = np.asarray(g, np.float64)
     r = np.asarray(r, np.float64)
     if g.shape != r.shape:
@@ -32,6 +49,8 @@ def parity_ok(g: np.ndarray, r: np.ndarray, rel: float = REL_TOL) -> tuple[bool,
     err = np.abs(g - r)
     normwise = err.max() / rmax if rmax > 0 else err.max()
     floor = rel * np.maximum(np.abs(r), rel * rmax)
+    if noise is not None:
+        floor = np.maximum(floor, np.asarray(noise, np.float64)[m][~inf])
     worst = np.max(err / np.maximum(floor, 1e-300)) if rmax > 0 else (0.0 if err.max() == 0 else np.inf)
     ok = (normwise <= rel) and bool(np.all(err <= floor)) if rmax > 0 else err.max() == 0
     return bool(ok), f"normwise={normwise:.3e} worst_elem_ratio={worst:.3f}"

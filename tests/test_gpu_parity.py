@@ -7,7 +7,7 @@ normwise ||g-r||_inf/||r||_inf <= 1e-3 and per element |g-r| <= 1e-3*max(|r|, 1e
 import numpy as np
 import pytest
 
-from _util import parity_ok, pattern_f32, pattern_src, random_acts, random_weights
+from _util import acc_noise, parity_ok, pattern_f32, pattern_src, random_acts, random_weights
 
 pytestmark = pytest.mark.gpu
 
@@ -26,6 +26,14 @@ def make_inputs(O, qt, M, K, N, kind="random", seed=0):
         raise ValueError("quantizeTensor needs numElements % 32 == 0")
     q = O.quantize(qt, src)
     return q, x
+
+
+def noise_for(O, qt, q, M, K, x):
+    """acc_noise for A = q (M x K blocks, flat-index layout) against x [K, N]; N > 1 runs on the
+    batched MFMA path and gets its activation-split bound too."""
+    w = np.abs(O.dequantize(qt, q, M * K)).reshape(M, K)
+    x = np.asarray(x).reshape(K, -1)
+    return acc_noise(w, np.abs(x), split=x.shape[1] > 1)
 
 
 def gpu_matmul(qt, q, M, K, N, x, a_off=0, b_off=0, d_off=0, dst_row_pad=0, b_stride=None, host=False):
@@ -67,8 +75,13 @@ SHAPES = [
     (17, 384, 1),     # 6 pairs per row (Q4_1 streams it: rows of 240 B)
     (16, 96, 1),      # K % 64 != 0 -> generic kernel
     (8, 40, 1),       # K % 32 != 0: blocks straddle rows (flat-index semantics)
-    (32, 128, 3),     # N > 1
+    (32, 128, 3),     # N > 1: MFMA GEMM (16-column tiles)
     (5, 256, 7),
+    (70, 96, 5),      # three blocks per row: a half K-stage
+    (100, 4096, 32),  # C3's batch: 32-column tiles
+    (33, 4352, 17),   # ragged rows and columns
+    (130, 512, 100),  # 64-column tiles, ragged
+    (8, 40, 3),       # K % 32 != 0 with N > 1: generic kernel
 ]
 
 
@@ -80,7 +93,7 @@ def test_mul_mat_vs_oracle(gpu, oracle, qt, shape, kind):
     q, x = make_inputs(oracle, qt, M, K, N, kind)
     ref = oracle.mat_mul_q(qt, q, M, K, x)
     got = gpu_matmul(qt, q, M, K, N, x)
-    ok, msg = parity_ok(got, ref)
+    ok, msg = parity_ok(got, ref, noise=noise_for(oracle, qt, q, M, K, x))
     assert ok, msg
 
 
@@ -264,8 +277,33 @@ def test_full_size_batch1_vs_oracle(gpu, oracle, qt, M, K):
     q, x = make_inputs(oracle, qt, M, K, 1, seed=M + K)
     ref = oracle.mat_mul_q(qt, q, M, K, x, tight=True)
     got = gpu_matmul(qt, q, M, K, 1, x)
-    ok, msg = parity_ok(got, ref)
+    ok, msg = parity_ok(got, ref, noise=noise_for(oracle, qt, q, M, K, x))
     assert ok, msg
+
+
+@pytest.mark.parametrize("qt,M,K,N", [(2, 11008, 4096, 32), (3, 11008, 4096, 32), (2, 4096, 11008, 32),
+                                      (6, 4096, 4096, 32)])
+def test_full_size_batched_vs_oracle(gpu, oracle, qt, M, K, N):
+    """BASELINE config C3 at batch 32 (and Q8_0 4096^2 at batch 32), full size."""
+    q, x = make_inputs(oracle, qt, M, K, N, seed=M + K + N)
+    ref = oracle.mat_mul_q(qt, q, M, K, x, tight=True)
+    got = gpu_matmul(qt, q, M, K, N, x)
+    ok, msg = parity_ok(got, ref, noise=noise_for(oracle, qt, q, M, K, x))
+    assert ok, msg
+
+
+def test_c5_prefill_rows_sampled(gpu, oracle):
+    """Config C5: Q4_0 4096 x 4096 x 512 on the GPU; the oracle checks 192 rows spread over M
+    (rows 0-63, a middle band and the last 64) — its full product would take minutes on one core."""
+    qt, M, K, N = 2, 4096, 4096, 512
+    q, x = make_inputs(oracle, qt, M, K, N, seed=5)
+    got = gpu_matmul(qt, q, M, K, N, x)
+    rb = K // 32 * 18
+    for r0 in (0, 2016, M - 64):
+        qs = q[r0 * rb:(r0 + 64) * rb]
+        ref = oracle.mat_mul_q(qt, qs, 64, K, x, tight=True)
+        ok, msg = parity_ok(got[r0:r0 + 64], ref, noise=noise_for(oracle, qt, qs, 64, K, x))
+        assert ok, (r0, msg)
 
 
 def test_full_size_linearity(gpu, oracle):

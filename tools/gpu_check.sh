@@ -16,6 +16,6 @@ step() {  # step <name> <seconds> <cmd...>
 [ -z "$NO_TESTS" ] && step pytest_gpu 900 python -m pytest tests -q -m gpu -x
 [ -n "$SMOKE" ] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 5
-[ -n "$PROF" ] && step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 20 --warmup 5 --no-headline --no-chain --no-cpu-baseline
+[ -n "$PROF" ] && step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 20 --warmup 5 --no-headline --no-chain --no-batched --no-cpu-baseline
 [ -n "$PROF" ] && grep -h "gemv\|Name" gpurun_out/prof_trace/run_kernel_stats.csv
 exit 0
