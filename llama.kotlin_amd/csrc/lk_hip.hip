@@ -313,11 +313,19 @@ int grow(void **p, size_t *have, size_t want) {
   return LK_OK;
 }
 
+int gemm_waves() {  // LK_GEMM_WAVES = 4 or 8 waves per LDS-GEMM workgroup (tuning only)
+  static int nw = [] {
+    const char *e = getenv("LK_GEMM_WAVES");
+    return (e && atoi(e) == 8) ? 8 : 4;
+  }();
+  return nw;
+}
+
 int gemm_occupancy() {  // LK_GEMM_OCC overrides (tuning only)
   static int occ = [] {
     const char *e = getenv("LK_GEMM_OCC");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 4;
+    return v > 0 ? v : 2;
   }();
   return occ;
 }
@@ -364,15 +372,15 @@ bool gemm_lds_eligible(int32_t qt, const lk_tensor *a, const Checked &c) {
   const uintptr_t base = (uintptr_t)a->data + a->data_offset;
   if (base % 8) return false;  // rows start 8-byte aligned for the 16-byte DMA pieces
   // the last row's last stage reads up to OVERREAD bytes past the matrix: they must be in the buffer
-  const uint64_t over = qt == LK_TYPE_Q4_0 ? LdsGemmGeom<LK_TYPE_Q4_0, 2>::OVERREAD
-                       : qt == LK_TYPE_Q4_1 ? LdsGemmGeom<LK_TYPE_Q4_1, 2>::OVERREAD
-                                            : LdsGemmGeom<LK_TYPE_Q8_0, 2>::OVERREAD;
+  const uint64_t over = qt == LK_TYPE_Q4_0 ? LdsGemmGeom<LK_TYPE_Q4_0, 2, 4>::OVERREAD
+                       : qt == LK_TYPE_Q4_1 ? LdsGemmGeom<LK_TYPE_Q4_1, 2, 4>::OVERREAD
+                                            : LdsGemmGeom<LK_TYPE_Q8_0, 2, 4>::OVERREAD;
   return c.a_hi + over <= a->buf_bytes;
 }
 
-template <int QT, int NT>
+template <int QT, int NT, int NW>
 int launch_gemm_lds_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
-  using GG = LdsGemmGeom<QT, NT>;
+  using GG = LdsGemmGeom<QT, NT, NW>;
   GemmScratch &S = gemm_scratch();
   g.tiles_m = (g.M + GG::BM - 1) / GG::BM;
   g.tiles_n = (g.N + GG::BN - 1) / GG::BN;
@@ -400,7 +408,7 @@ int launch_gemm_lds_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
   const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
   hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
   constexpr size_t lds = GG::LDS;
-  hipLaunchKernelGGL((gemm_q_lds_kernel<QT, NT>), dim3((unsigned)(tiles * slices)), dim3(256), lds, st, g);
+  hipLaunchKernelGGL((gemm_q_lds_kernel<QT, NT, NW>), dim3((unsigned)(tiles * slices)), dim3(NW * 64), lds, st, g);
   HIP_TRY(hipGetLastError());
   return LK_OK;
 }
@@ -408,9 +416,10 @@ int launch_gemm_lds_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
 template <int QT>
 int launch_gemm_qt(const GemmArgs &g, const XSplitArgs &xa, bool lds_ok, hipStream_t st) {
   if (lds_ok) {
-    if (g.N <= 16) return launch_gemm_lds_t<QT, 1>(g, xa, st);
-    if (g.N <= 32) return launch_gemm_lds_t<QT, 2>(g, xa, st);
-    return launch_gemm_lds_t<QT, 4>(g, xa, st);
+    const int nw = gemm_waves();
+    if (g.N <= 16) return nw == 8 ? launch_gemm_lds_t<QT, 1, 8>(g, xa, st) : launch_gemm_lds_t<QT, 1, 4>(g, xa, st);
+    if (g.N <= 32) return nw == 8 ? launch_gemm_lds_t<QT, 2, 8>(g, xa, st) : launch_gemm_lds_t<QT, 2, 4>(g, xa, st);
+    return nw == 8 ? launch_gemm_lds_t<QT, 4, 8>(g, xa, st) : launch_gemm_lds_t<QT, 4, 4>(g, xa, st);
   }
   if (g.N <= 16) return launch_gemm_t<QT, 4, 1, 2, 1>(g, xa, st);
   if (g.N <= 32) return launch_gemm_t<QT, 4, 1, 2, 2>(g, xa, st);

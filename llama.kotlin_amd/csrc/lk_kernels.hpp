@@ -880,9 +880,9 @@ __device__ __forceinline__ void dma16(const void *sbase, uint32_t vofs, const vo
 }
 #pragma clang diagnostic pop
 
-// LDS-DMA pipelined variant: 4 waves stacked along M (wave tile: MT = 2 weight tiles × NT
-// x-tiles; BM = 128, BN = 16·NT), K in stages of SB = 4 blocks. Each stage — the workgroup's
-// 128 rows × 4 blocks of raw weight bytes (rounded up to 16-byte pieces; rows then start
+// LDS-DMA pipelined variant: NW waves stacked along M (wave tile: MT = 2 weight tiles × NT
+// x-tiles; BM = 32·NW, BN = 16·NT), K in stages of SB = 4 blocks. Each stage — the workgroup's
+// BM rows × 4 blocks of raw weight bytes (rounded up to 16-byte pieces; rows then start
 // 8-byte aligned), the 4·NT·2 activation fragments (1 KB each) and the T sums — moves
 // global -> LDS by LDS-DMA into a ring of D stages. Every wave issues the same number of DMA
 // instructions per stage, so a counted vmcnt plus one barrier publishes a stage, and D-1 stages
@@ -890,16 +890,18 @@ __device__ __forceinline__ void dma16(const void *sbase, uint32_t vofs, const vo
 // launch; only the SGPR bases move with the stage.
 constexpr int kLdsSB = 4;
 
-template <int QT, int NT> struct LdsGemmGeom {
+template <int QT, int NT, int NW> struct LdsGemmGeom {
   static constexpr int BB = QTraits<QT>::BB;
   static constexpr int SB = kLdsSB;
-  static constexpr int MT = 2, BM = 128, BN = 16 * NT;
+  static constexpr int MT = 2, BM = NW * MT * 16, BN = 16 * NT;
   static constexpr int AROWP = (SB * BB + 15) / 16 * 16;   // LDS bytes per row per stage
   static constexpr int A_INST = BM * (AROWP / 16) / 64;     // DMA instructions for A
   static constexpr int X_INST = SB * NT * kXSplits;
   static constexpr int T_INST = GemmQ<QT>::USES_T ? 1 : 0;
-  static constexpr int NINST = A_INST + X_INST + T_INST;
-  static constexpr int C = (NINST + 3) / 4;                 // per wave per stage (padded)
+  // per wave per stage: each kind padded to a multiple of the NW waves, so that a wave's c-th
+  // instruction has a compile-time kind (A: c < CA, X: c < CA + CX, T: the rest)
+  static constexpr int CA = (A_INST + NW - 1) / NW, CX = (X_INST + NW - 1) / NW, CT = (T_INST + NW - 1) / NW;
+  static constexpr int C = CA + CX + CT;
   static constexpr int A_BYTES = BM * AROWP;
   static constexpr int X_BYTES = X_INST * 1024;
   static constexpr int T_BYTES = T_INST * 1024;
@@ -914,9 +916,9 @@ template <int QT, int NT> struct LdsGemmGeom {
   static_assert((D - 1) * C < 64, "vmcnt");
 };
 
-template <int QT, int NT>
-__global__ __launch_bounds__(256) void gemm_q_lds_kernel(GemmArgs g) {
-  using G = LdsGemmGeom<QT, NT>;
+template <int QT, int NT, int NW>
+__global__ __launch_bounds__(NW * 64) void gemm_q_lds_kernel(GemmArgs g) {
+  using G = LdsGemmGeom<QT, NT, NW>;
   using Q = GemmQ<QT>;
   constexpr int MT = G::MT, BM = G::BM, BN = G::BN, BB = G::BB, SB = G::SB;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -933,29 +935,33 @@ __global__ __launch_bounds__(256) void gemm_q_lds_kernel(GemmArgs g) {
   const int ntx = (g.N + 15) / 16;
   const int n16 = ntx * 16;
 
-  // This wave's DMA instructions q = wave·C + c (padding repeats the last): kind (0 A, 1 X, 2 T),
-  // per-lane byte offset from the kind's stage base, and LDS byte offset within a stage.
+  // This wave's DMA instructions: slot c < CA moves A piece-instruction min(wave·CA + c, A_INST-1),
+  // CA <= c < CA+CX the X fragment min(wave·CX + c', X_INST-1), the last CT the T sums (padding
+  // repeats an instruction: same bytes to the same place). Per lane: the byte offset from the
+  // kind's stage base (fixed for the launch) and the LDS byte offset within a stage (uniform).
   uint32_t vofs[G::C];
-  int kind[G::C], ldso[G::C];
+  int ldso[G::C];
 #pragma unroll
   for (int c = 0; c < G::C; c++) {
-    const int q = min(wave * G::C + c, G::NINST - 1);
-    if (q < G::A_INST) {
+    if (c < G::CA) {
+      const int q = min(wave * G::CA + c, G::A_INST - 1);
       const int piece = q * 64 + lane;
       const int r = piece / (G::AROWP / 16), pc = piece % (G::AROWP / 16);
       const int64_t row = min((int64_t)tm * BM + r, (int64_t)g.M - 1);
-      kind[c] = 0; vofs[c] = (uint32_t)(row * RB + pc * 16); ldso[c] = q * 1024;
-    } else if (q < G::A_INST + G::X_INST) {
-      const int x = q - G::A_INST;  // (block b, tile j, split sp)
+      vofs[c] = (uint32_t)(row * RB + pc * 16);
+      ldso[c] = q * 1024;
+    } else if (c < G::CA + G::CX) {
+      const int x = min(wave * G::CX + (c - G::CA), G::X_INST - 1);  // (block b, tile j, split sp)
       const int b = x / (NT * kXSplits), j = (x / kXSplits) % NT, sp = x % kXSplits;
       const int xt = min(tn * NT + j, ntx - 1);
-      kind[c] = 1; vofs[c] = (uint32_t)((((int64_t)xt * nblk + b) * kXSplits + sp) * 1024 + lane * 16);
+      vofs[c] = (uint32_t)((((int64_t)xt * nblk + b) * kXSplits + sp) * 1024 + lane * 16);
       ldso[c] = G::A_BYTES + x * 1024;
     } else {
       const int li = min(lane, SB * BN / 4 - 1);  // lane -> (block li / (BN/4), 4 columns)
       const int b = li / (BN / 4), c4 = li % (BN / 4);
       const int n = min(tn * BN + 4 * c4, n16 - 4);
-      kind[c] = 2; vofs[c] = (uint32_t)(((int64_t)b * n16 + n) * 4); ldso[c] = G::A_BYTES + G::X_BYTES;
+      vofs[c] = (uint32_t)(((int64_t)b * n16 + n) * 4);
+      ldso[c] = G::A_BYTES + G::X_BYTES;
     }
   }
   auto issue_stage = [&](int st, int sl) __attribute__((always_inline)) {
@@ -966,9 +972,9 @@ __global__ __launch_bounds__(256) void gemm_q_lds_kernel(GemmArgs g) {
     uint8_t *slot = smem + sl * G::STAGE;
 #pragma unroll
     for (int c = 0; c < G::C; c++) {
-      const uint8_t *base = kind[c] == 0 ? base_a : kind[c] == 1 ? base_x : base_t;
-      if (kind[c] == 0) dma16<LK_WEIGHT_AUX == 2>(base, vofs[c], slot + ldso[c]);
-      else dma16<false>(base, vofs[c], slot + ldso[c]);
+      if (c < G::CA) dma16<LK_WEIGHT_AUX == 2>(base_a, vofs[c], slot + ldso[c]);
+      else if (c < G::CA + G::CX) dma16<false>(base_x, vofs[c], slot + ldso[c]);
+      else dma16<false>(base_t, vofs[c], slot + ldso[c]);
     }
   };
 
@@ -987,8 +993,8 @@ __global__ __launch_bounds__(256) void gemm_q_lds_kernel(GemmArgs g) {
       const uint8_t *A = smem + slot * G::STAGE;
       const uint8_t *X = A + G::A_BYTES;
       const float *T = (const float *)(X + G::X_BYTES);
-#pragma unroll
-      for (int b = 0; b < SB; b++) {
+#pragma unroll 1
+      for (int b = 0; b < SB; b++) {  // not unrolled: keeps the fragment reads of one block live
         bf16x8 wf[MT];
         float s1[MT], s2[MT];
 #pragma unroll
