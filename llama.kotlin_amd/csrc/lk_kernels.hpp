@@ -268,7 +268,8 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 #ifndef LK_WEIGHT_AUX
 #define LK_WEIGHT_AUX 2
 #endif
-// Prologue order: 0 = activations then D weight units; 1 = weight unit 0, activations, units 1..D-1.
+// Prologue order: 0 = activations then D weight units; 1 = weight unit 0, activations, units 1..D-1;
+// 2 = activations, wait for them, then the D weight units.
 #ifndef LK_PROLOGUE_ORDER
 #define LK_PROLOGUE_ORDER 0
 #endif
@@ -490,8 +491,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(xv + p * 16 + t), (LK_LDS void *)(lds + k * 64), 16, 0, 0);
       }
     };
-    __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
-    if (LK_PROLOGUE_ORDER == 0) dma_x();
+    if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
+    if (LK_PROLOGUE_ORDER == 0 || LK_PROLOGUE_ORDER == 2) dma_x();
+    if (LK_PROLOGUE_ORDER == 2) {  // the image first, alone: its latency is not queued behind the weight burst
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+    }
 #pragma unroll
     for (int k = 0; k < G::D; k++) {
       if (LK_PROLOGUE_ORDER == 1 && k == 1) dma_x();
@@ -506,8 +511,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     }
     islot = 0;  // the next unit to issue is unit D, slot D % D
 
-    wait_vmcnt<(LK_PROLOGUE_ORDER == 0 ? G::D : G::D - 1) * G::L>();  // this wave's activation DMA has landed
-    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    if (LK_PROLOGUE_ORDER != 2) {
+      wait_vmcnt<(LK_PROLOGUE_ORDER == 0 ? G::D : G::D - 1) * G::L>();  // this wave's activation DMA has landed
+      __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    }
 
     // 2. activations into VGPRs in decode order, and Σx per block
     f32x4 xr[CPL][16];

@@ -42,15 +42,15 @@ __global__ void x0_read(const f32x4 *__restrict__ p, size_t n4, float *out) {
 }
 
 // row of the i-th unit of (workgroup g, wave w); returns -1 past the end
-template <int MODE>
+template <int MODE, int NW = 8>
 __device__ __forceinline__ int row_of(int i, int g, int w, int G, int M) {
   if (MODE == 0) {
     const int per_wg = (M + G - 1) / G, r0 = g * per_wg, r1 = min(r0 + per_wg, M);
-    const int per_w = (max(r1 - r0, 0) + 7) / 8;
+    const int per_w = (max(r1 - r0, 0) + NW - 1) / NW;
     const int r = r0 + w * per_w + i;
     return (i < per_w && r < r1) ? r : -1;
   } else if (MODE == 1) {
-    const int r = (g * 8 + w) + i * G * 8;
+    const int r = (g * NW + w) + i * G * NW;
     return r < M ? r : -1;
   } else {
     const int per_wg = (M + G - 1) / G, r0 = g * per_wg, r1 = min(r0 + per_wg, M);
@@ -59,8 +59,8 @@ __device__ __forceinline__ int row_of(int i, int g, int w, int G, int M) {
   }
 }
 
-template <int MODE, bool DECODE, int D, bool BATCH = false, int AUX = 0>
-__global__ __launch_bounds__(512) void s_kernel(const uint8_t *__restrict__ a, const float *__restrict__ x, float *__restrict__ dst,
+template <int MODE, bool DECODE, int D, bool BATCH = false, int AUX = 0, int NW = 8, bool NOX = false>
+__global__ __launch_bounds__(NW * 64) void s_kernel(const uint8_t *__restrict__ a, const float *__restrict__ x, float *__restrict__ dst,
                                                 int M) {
   extern __shared__ f32x4 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -77,13 +77,13 @@ __global__ __launch_bounds__(512) void s_kernel(const uint8_t *__restrict__ a, c
     }
   };
   // activations (natural, swizzled) by DMA
-  for (int k = wave; k < NP / 4; k += 8) {
+  for (int k = wave; k < (NOX ? 0 : NP / 4); k += NW) {
     const int i = k * 64 + lane, p = i >> 4, t = (i & 15) ^ (p & 15);
     __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)((const f32x4 *)x + p * 16 + t),
                                      (__attribute__((address_space(3))) void *)(lds + k * 64), 16, 0, 0);
   }
 #pragma unroll
-  for (int k = 0; k < D; k++) dma(row_of<MODE>(k, g, wave, G, M), k);
+  for (int k = 0; k < D; k++) dma(row_of<MODE, NW>(k, g, wave, G, M), k);
   lk::wait_vmcnt<D * L>();
   __builtin_amdgcn_s_barrier();
   f32x4 xr[16];
@@ -101,9 +101,9 @@ __global__ __launch_bounds__(512) void s_kernel(const uint8_t *__restrict__ a, c
   float outv = 0.f;
   int rows_seen[1] = {0};
   for (int i = 0;; i++) {
-    const int r = row_of<MODE>(i, g, wave, G, M);
+    const int r = row_of<MODE, NW>(i, g, wave, G, M);
     if (r < 0) break;
-    const bool more = row_of<MODE>(i + D - 1, g, wave, G, M) >= 0;
+    const bool more = row_of<MODE, NW>(i + D - 1, g, wave, G, M) >= 0;
     if (more) lk::wait_vmcnt<(D - 1) * L>();
     else lk::wait_vmcnt<0>();
     const uint32_t *rp = (const uint32_t *)(ring + slot * SLOT + lane * 36);
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(512) void s_kernel(const uint8_t *__restrict__ a, c
     float v = 0.f;
     if (DECODE) v = lk::pair_dot_s<LK_TYPE_Q4_0>(w, xr, xs0, xs1);
     else v = __builtin_bit_cast(float, w[0] ^ w[4] ^ w[8]);
-    const int rn = row_of<MODE>(i + D, g, wave, G, M);
+    const int rn = row_of<MODE, NW>(i + D, g, wave, G, M);
     if (rn >= 0) {
       lk::wait_lgkmcnt0();
       dma(rn, slot);
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(512) void s_kernel(const uint8_t *__restrict__ a, c
       // hold row i's total in lane i % 64; one store per 64 rows (row index of lane l kept in rsl)
       const float tv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), 63));
       if (lane == (i & 63)) { outv = tv; rows_seen[0] = r; }
-      const bool last = row_of<MODE>(i + 1, g, wave, G, M) < 0;
+      const bool last = row_of<MODE, NW>(i + 1, g, wave, G, M) < 0;
       if ((i & 63) == 63 || last) {
         if (lane <= (i & 63)) dst[rows_seen[0]] = outv;
       }
@@ -172,7 +172,28 @@ int main(int argc, char **argv) {
   timeit(#DEC " m=" #MODE " D=" #D " batch=" #B " aux=" #AUX, [&] {                                                  \
     hipLaunchKernelGGL((s_kernel<MODE, DEC, D, B, AUX>), dim3(256), dim3(512), NP * 256 + 8 * D * SLOT, 0, a, x, d, M); \
   })
-  RUN(0, false, 3, false, 0); RUN(0, false, 3, false, 2); RUN(0, false, 5, false, 2);
-  RUN(0, true, 3, false, 0); RUN(0, true, 3, false, 2); RUN(0, true, 5, false, 2); RUN(2, true, 3, false, 2);
+  auto prod = [&](const char *name) {
+    timeit(name, [&] {
+      lk::GemvDesc gd{};
+      gd.a = a; gd.x = x; gd.dst = d; gd.dst_row_stride = 1; gd.M = M; gd.K = K;
+      constexpr size_t plds = lk::StreamGeom<LK_TYPE_Q4_0, 1>::LDS;
+      hipLaunchKernelGGL((lk::gemv_stream_kernel<LK_TYPE_Q4_0, 1>), dim3(256), dim3(512), plds, 0, gd,
+                         (const lk::StreamWork *)nullptr, 0);
+    });
+  };
+#define RUNW(NW, D, G)                                                                                          \
+  timeit("decode NW=" #NW " D=" #D " grid=" #G, [&] {                                                          \
+    hipLaunchKernelGGL((s_kernel<0, true, D, false, 2, NW>), dim3(G), dim3(NW * 64), NP * 256 + NW * D * SLOT, 0, a, x, d, M); \
+  })
+  for (int rep = 0; rep < 2; rep++) {
+    RUNW(8, 3, 256);
+    timeit("decode NW=8 D=3 no-x (timing only)", [&] {
+      hipLaunchKernelGGL((s_kernel<0, true, 3, false, 2, 8, true>), dim3(256), dim3(512), NP * 256 + 8 * 3 * SLOT, 0, a, x, d, M);
+    });
+    timeit("dma-only NW=8 D=3 no-x", [&] {
+      hipLaunchKernelGGL((s_kernel<0, false, 3, false, 2, 8, true>), dim3(256), dim3(512), NP * 256 + 8 * 3 * SLOT, 0, a, x, d, M);
+    });
+    prod("production gemv_stream<Q4_0,1>");
+  }
   return 0;
 }
