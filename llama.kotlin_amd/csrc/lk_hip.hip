@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "lk_kernels.hpp"
+#include "../../include/lk_gguf.h"
 
 using namespace lk;
 
@@ -43,6 +44,13 @@ int fail(int st, const char *fmt, ...) {
     hipError_t e_ = (expr);                                                                    \
     if (e_ != hipSuccess) return fail(LK_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
+
+}  // namespace
+
+// shared with lk_gguf.cpp (one lk_last_error for the whole library)
+int lk_detail_fail(int st, const char *msg) { return fail(st, "%s", msg); }
+
+namespace {
 
 struct State {
   std::mutex mu;
@@ -825,6 +833,29 @@ int lk_quantize_device(const float *src, int64_t n, int32_t type, void *out, voi
     case LK_TYPE_Q4_0: hipLaunchKernelGGL(quantize_kernel<LK_TYPE_Q4_0>, grid, block, 0, st, src, (uint8_t *)out, nblk); break;
     case LK_TYPE_Q4_1: hipLaunchKernelGGL(quantize_kernel<LK_TYPE_Q4_1>, grid, block, 0, st, src, (uint8_t *)out, nblk); break;
     default: hipLaunchKernelGGL(quantize_kernel<LK_TYPE_Q8_0>, grid, block, 0, st, src, (uint8_t *)out, nblk); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+int lk_repack_q4_device(void *blocks, int64_t n_blocks, int32_t type, int32_t direction, void *stream) {
+  if (type != LK_TYPE_Q4_0 && type != LK_TYPE_Q4_1)
+    return fail(LK_ERR_NOT_IMPLEMENTED, "repack: type %d has no nibble-order variant", type);
+  if (direction != LK_REPACK_UPSTREAM_TO_KOTLIN && direction != LK_REPACK_KOTLIN_TO_UPSTREAM)
+    return fail(LK_ERR_INVALID_ARG, "repack: direction %d", direction);
+  if (n_blocks < 0) return fail(LK_ERR_INVALID_ARG, "repack: n_blocks %lld", (long long)n_blocks);
+  if (n_blocks == 0) return LK_OK;
+  if (!blocks) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
+  if ((uintptr_t)blocks & 1) return fail(LK_ERR_INVALID_ARG, "repack: blocks not 2-byte aligned");
+  hipStream_t st = pick_stream(stream);
+  uint8_t *p = (uint8_t *)blocks;
+  dim3 grid((unsigned)((n_blocks + 255) / 256)), block(256);
+  if (type == LK_TYPE_Q4_0) {
+    if (direction == 0) hipLaunchKernelGGL((repack_q4_kernel<LK_TYPE_Q4_0, 0>), grid, block, 0, st, p, n_blocks);
+    else hipLaunchKernelGGL((repack_q4_kernel<LK_TYPE_Q4_0, 1>), grid, block, 0, st, p, n_blocks);
+  } else {
+    if (direction == 0) hipLaunchKernelGGL((repack_q4_kernel<LK_TYPE_Q4_1, 0>), grid, block, 0, st, p, n_blocks);
+    else hipLaunchKernelGGL((repack_q4_kernel<LK_TYPE_Q4_1, 1>), grid, block, 0, st, p, n_blocks);
   }
   HIP_TRY(hipGetLastError());
   return LK_OK;

@@ -1126,6 +1126,41 @@ __global__ __launch_bounds__(256) void dequantize_kernel(const uint8_t *__restri
   }
 }
 
+// GGUF nibble-order conversion (include/lk_gguf.h), in place, one thread per block.
+// Upstream byte j = w[j] | w[j+16] << 4 (ggml-quants.c:1515-1553); llama.kotlin byte
+// j = w[2j] | w[2j+1] << 4 (GGMLTypes.kt:647-651). Scale/min bytes are untouched.
+// A wave covers 64 consecutive blocks (1152/1280 contiguous bytes): HBM-bound, 2x the
+// nibble bytes of traffic per block.
+template <int QT, int DIR>
+__global__ __launch_bounds__(256) void repack_q4_kernel(uint8_t *__restrict__ blocks, int64_t nblk) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  uint16_t *q = (uint16_t *)(blocks + b * QTraits<QT>::BB + (QT == LK_TYPE_Q4_1 ? 4 : 2));
+  uint8_t in[16], o[16];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint32_t v = q[j];
+    in[2 * j] = (uint8_t)v;
+    in[2 * j + 1] = (uint8_t)(v >> 8);
+  }
+  if constexpr (DIR == 0) {  // upstream -> kotlin
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      o[j] = (uint8_t)((in[2 * j] & 0x0F) | (in[2 * j + 1] << 4));
+      o[j + 8] = (uint8_t)((in[2 * j] >> 4) | (in[2 * j + 1] & 0xF0));
+    }
+  } else {  // kotlin -> upstream: w[j] = nibble (j&1) of byte j>>1
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t lo = (in[j >> 1] >> ((j & 1) * 4)) & 0xF;
+      const uint32_t hi = (in[8 + (j >> 1)] >> ((j & 1) * 4)) & 0xF;
+      o[j] = (uint8_t)(lo | (hi << 4));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) q[j] = (uint16_t)(o[2 * j] | (o[2 * j + 1] << 8));
+}
+
 // kotlin maxOf / minOf on Float: NaN-propagating, -0.0 < +0.0.
 __device__ __forceinline__ float kmax(float a, float b) {
   if (__builtin_isnan(a) || __builtin_isnan(b)) return __builtin_nanf("");

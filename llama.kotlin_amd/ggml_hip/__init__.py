@@ -8,6 +8,7 @@ C-ABI in include/lk_hip.h (liblk_hip.so, hand-written HIP kernels):
   GGMLHipBackend (GGMLBackend)                        core/GGMLBackend.kt:90-157
   dequantizeTensor / quantizeTensor (device)          core/GGMLComputeOps.kt:918 / :1040
   RowShardedMulMat (rows over GPUs + RCCL gather)     new: the reference is single-device
+  GGUFParser / ModelLoader / LoadedModel              gguf/GGUFParser.kt, gguf/ModelLoader.kt
 
 There is no CPU compute path in this package: a missing liblk_hip.so raises.
 """
@@ -17,6 +18,7 @@ from ._lib import (HipDeviceError, IllegalArgumentException, IllegalStateExcepti
 from .backend import GGMLBackendRegistry, GGMLHipBackend, GGMLStatus
 from .ops import (MulMatPlan, computeMatMul, dequantizeTensor, quantizeTensor, to_lk, validateMatMul, weightsEvictAll,
                   weightsPin)
+from .gguf import GGUFContext, GGUFParser, GGUFTensorInfo, GGUFType, LoadedModel, ModelLoader
 from .sharded import RowShardedMulMat, row_slice, shard_rows
 from .tensor import (GGMLCGraph, GGMLContext, GGMLGraphAllocator, GGMLOp, GGMLTensor, GGMLType,
                      calculateContiguousStrides, calculateTensorByteSize)
@@ -28,6 +30,7 @@ __all__ = [
     "weightsEvictAll", "to_lk",
     "GGMLHipBackend", "GGMLStatus", "GGMLBackendRegistry",
     "RowShardedMulMat", "row_slice", "shard_rows",
+    "GGUFParser", "GGUFContext", "GGUFTensorInfo", "GGUFType", "ModelLoader", "LoadedModel",
     "IllegalArgumentException", "IndexOutOfBoundsException", "IllegalStateException", "NotOffloadedError",
     "HipDeviceError",
 ]

@@ -77,6 +77,12 @@ EXPORTED_SYMBOLS = (
     "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy",
     "lk_weights_pin", "lk_weights_evict_all", "lk_weights_cached_bytes",
     "lk_dequantize_device", "lk_quantize_device",
+    # include/lk_gguf.h
+    "lk_gguf_open_memory", "lk_gguf_open_file", "lk_gguf_close", "lk_gguf_version", "lk_gguf_alignment",
+    "lk_gguf_data_offset", "lk_gguf_data_bytes", "lk_gguf_kv_count", "lk_gguf_find_key", "lk_gguf_kv_key",
+    "lk_gguf_kv_type", "lk_gguf_kv_array_info", "lk_gguf_kv_get", "lk_gguf_kv_array_data",
+    "lk_gguf_kv_get_string", "lk_gguf_tensor_count", "lk_gguf_find_tensor", "lk_gguf_get_tensor_info",
+    "lk_gguf_tensor_data", "lk_gguf_load_tensor", "lk_gguf_load_all_device", "lk_repack_q4_device",
 )
 
 _lib = None
@@ -116,6 +122,36 @@ def load():
     L.lk_weights_cached_bytes.restype = ctypes.c_uint64
     L.lk_dequantize_device.argtypes = [P, vp, vp]
     L.lk_quantize_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp]
+    # GGUF (include/lk_gguf.h); handles are opaque void*
+    u64, i64, i32, pvp, pu64 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)
+    L.lk_gguf_open_memory.argtypes = [vp, u64, i32, pvp]
+    L.lk_gguf_open_file.argtypes = [ctypes.c_char_p, i32, pvp]
+    L.lk_gguf_close.argtypes = [vp]
+    L.lk_gguf_close.restype = None
+    L.lk_gguf_version.argtypes = [vp]
+    L.lk_gguf_version.restype = ctypes.c_uint32
+    for f in (L.lk_gguf_alignment, L.lk_gguf_data_offset, L.lk_gguf_data_bytes):
+        f.argtypes = [vp]
+        f.restype = u64
+    for f in (L.lk_gguf_kv_count, L.lk_gguf_tensor_count):
+        f.argtypes = [vp]
+        f.restype = i64
+    for f in (L.lk_gguf_find_key, L.lk_gguf_find_tensor):
+        f.argtypes = [vp, ctypes.c_char_p]
+        f.restype = i64
+    L.lk_gguf_kv_key.argtypes = [vp, i64]
+    L.lk_gguf_kv_key.restype = ctypes.c_char_p
+    L.lk_gguf_kv_type.argtypes = [vp, i64]
+    L.lk_gguf_kv_type.restype = i32
+    L.lk_gguf_kv_array_info.argtypes = [vp, i64, ctypes.POINTER(i32), pu64]
+    L.lk_gguf_kv_get.argtypes = [vp, i64, i64, vp, u64]
+    L.lk_gguf_kv_array_data.argtypes = [vp, i64, pvp, pu64]
+    L.lk_gguf_kv_get_string.argtypes = [vp, i64, i64, pvp, pu64]
+    L.lk_gguf_get_tensor_info.argtypes = [vp, i64, vp]
+    L.lk_gguf_tensor_data.argtypes = [vp, i64, pvp, pu64]
+    L.lk_gguf_load_tensor.argtypes = [vp, i64, vp, u64, i32, vp]
+    L.lk_gguf_load_all_device.argtypes = [vp, vp, u64, vp]
+    L.lk_repack_q4_device.argtypes = [vp, i64, i32, i32, vp]
     _lib = L
     return L
 

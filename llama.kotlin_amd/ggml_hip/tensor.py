@@ -228,11 +228,15 @@ class GGMLGraphAllocator:
         new[: self.bufferSize(bufferId)] = old
         self.buffers[bufferId] = new
 
-    def allocateTensor(self, type_: GGMLType, ne, bufferId: int = 0, name: str = "") -> GGMLTensor:
-        """core/GGMLAlloc.kt:486-499: a leaf tensor with contiguous strides in buffer bufferId."""
+    def allocateTensor(self, type_: GGMLType, ne, bufferId: int = 0, name: str = "",
+                       nbytes: int | None = None) -> GGMLTensor:
+        """core/GGMLAlloc.kt:486-499: a leaf tensor with contiguous strides in buffer bufferId.
+
+        ``nbytes`` overrides calculateTensorByteSize for storage it does not size (the
+        K-quant and Q5/Q8_1 blocks a GGUF file can hold)."""
         ne = list(ne) + [1] * (GGML_MAX_DIMS - len(ne))
         t = GGMLTensor(type_, ne, name=name)
-        size = calculateTensorByteSize(t)
+        size = calculateTensorByteSize(t) if nbytes is None else int(nbytes)
         off = (self._tops[bufferId] + self.ALIGNMENT - 1) // self.ALIGNMENT * self.ALIGNMENT
         if off + size > self.bufferSize(bufferId):
             self.reserve(max(off + size, 2 * self.bufferSize(bufferId)), bufferId)

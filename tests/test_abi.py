@@ -12,13 +12,16 @@ import pytest
 from _util import pattern_f32, pattern_src
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "lk_hip.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("lk_hip.h", "lk_gguf.h")]
 
 
 def header_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(lk_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(lk_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +36,7 @@ def test_exports_every_declared_symbol(lib):
     names = header_functions()
     assert len(names) >= 15
     for n in names:
-        assert hasattr(lib, n), f"{n} declared in lk_hip.h but not exported"
+        assert hasattr(lib, n), f"{n} declared in include/ but not exported"
     import ggml_hip._lib as L
     assert set(L.EXPORTED_SYMBOLS) == set(names)
 
