@@ -22,6 +22,9 @@
  *                         are resident; core/GGMLBackend.kt:146).
  *   lk_plan_*             core/GGMLBackend.kt:146 graphCompute(graph) over a graph whose
  *                         MUL_MAT nodes are mutually independent: one launch for the set.
+ *   lk_mul_mat_sharded    SURVEY §8b's sharded entry: computeMatMul with A's rows split
+ *                         over the GPUs of one node from one host thread (the reference
+ *                         is single-device; this is the north star's row sharding).
  *   lk_weights_pin/evict  residency cache behind GGMLBackendBuffer.setTensor
  *                         (core/GGMLBackend.kt:63-69) for host-authoritative ByteArrays.
  *   lk_dequantize_device  core/GGMLComputeOps.kt:918 dequantizeTensor (Q8_0/Q4_0/Q4_1).
@@ -137,6 +140,14 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst);
  * launch; no allocation, no host synchronisation (graph-capturable). */
 int lk_mul_mat_device(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, void *stream);
 
+/* computeMatMul over HOST buffers with A's rows split into n_shards equal row ranges
+ * (ceil(M/n_shards) rows each), shard r computed on device r mod lk_device_count().
+ * Each shard writes its own rows of dst back into dst->data (the in-process all-gather);
+ * results meet lk_mul_mat's parity bar (bit-identical to it at N = 1, where every row is
+ * one wave's sequential sum). Falls back to one device when rows are not byte
+ * ranges (quantized A with K % 32 != 0) or dst rows interleave. Synchronous. */
+int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, int n_shards);
+
 /* ---- grouped execution of independent MUL_MAT nodes ------------------------ */
 
 typedef struct lk_plan lk_plan;
@@ -158,6 +169,9 @@ int lk_weights_pin(const lk_tensor *a, uint64_t generation);
 void lk_weights_evict_all(void);
 /* Bytes currently held by the weight cache. */
 uint64_t lk_weights_cached_bytes(void);
+/* Pin each row shard of a quantized A on the device lk_mul_mat_sharded(…, n_shards)
+ * runs it on (the mirror lk_weights_pin keeps, per shard and device). */
+int lk_weights_pin_sharded(const lk_tensor *a, uint64_t generation, int n_shards);
 
 /* ---- format kernels (the steps either side of the path) --------------------- */
 

@@ -52,21 +52,29 @@ int lk_detail_fail(int st, const char *msg) { return fail(st, "%s", msg); }
 
 namespace {
 
-struct State {
-  std::mutex mu;
-  int device = -1;
+// Per-device state of the host (ByteArray) path: one library stream, the weight
+// residency cache and staging scratch. lk_mul_mat uses the current device;
+// lk_mul_mat_sharded drives several from one host thread.
+constexpr int kMaxDevices = 64;
+struct Dev {
   hipStream_t stream = nullptr;
   // weight residency cache (host path): key = (host base, offset, bytes, generation)
   std::map<std::tuple<uintptr_t, uint64_t, uint64_t, uint64_t>, void *> weights;
   uint64_t weight_bytes = 0;
-  // scratch for the host path
+  // scratch for the host path: A staging, B, dst span
   void *scratch[3] = {nullptr, nullptr, nullptr};
   size_t scratch_bytes[3] = {0, 0, 0};
+};
+struct State {
+  std::mutex mu;
+  int device = -1;  // the device lk_mul_mat / lk_weights_pin use
+  Dev devs[kMaxDevices];
 };
 State &S() {
   static State s;
   return s;
 }
+Dev &cur() { return S().devs[S().device < 0 ? 0 : S().device]; }
 
 int block_bytes(int32_t t) {
   switch (t) {
@@ -518,8 +526,7 @@ int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *ds
   return launch_generic(a, b, dst, c, st);
 }
 
-int ensure_scratch(int idx, size_t bytes) {
-  State &s = S();
+int ensure_scratch(Dev &s, int idx, size_t bytes) {
   if (s.scratch_bytes[idx] >= bytes) return LK_OK;
   if (s.scratch[idx]) HIP_TRY(hipFree(s.scratch[idx]));
   s.scratch[idx] = nullptr;
@@ -535,8 +542,37 @@ int ensure_scratch(int idx, size_t bytes) {
 int ensure_init() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  if (S().stream && S().device == dev) return LK_OK;
+  if (S().device == dev && S().devs[dev].stream) return LK_OK;
   return lk_init(dev);
+}
+
+// The library stream of device d (created on first use); leaves d current.
+int init_dev(int d) {
+  HIP_TRY(hipSetDevice(d));
+  Dev &v = S().devs[d];
+  if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+  return LK_OK;
+}
+
+// Device mirror of host bytes [lo, hi) of base if a pinned range covers them.
+const void *find_pinned(Dev &v, const void *base, uint64_t lo, uint64_t hi) {
+  for (auto &kv : v.weights) {
+    auto [b, off, bytes, gen] = kv.first;
+    (void)gen;
+    if (b == (uintptr_t)base && off <= lo && hi <= off + bytes) return (const uint8_t *)kv.second + (lo - off);
+  }
+  return nullptr;
+}
+
+int pin_on(Dev &v, const lk_tensor *a, uint64_t lo, uint64_t bytes, uint64_t generation) {
+  auto key = std::make_tuple((uintptr_t)a->data, lo, bytes, generation);
+  if (v.weights.count(key)) return LK_OK;
+  void *dev = nullptr;
+  HIP_TRY(hipMalloc(&dev, std::max<uint64_t>(bytes, 4)));
+  HIP_TRY(hipMemcpy(dev, (const uint8_t *)a->data + lo, bytes, hipMemcpyHostToDevice));
+  v.weights[key] = dev;
+  v.weight_bytes += bytes;
+  return LK_OK;
 }
 
 }  // namespace
@@ -560,38 +596,49 @@ int lk_device_count(void) {
 int lk_init(int device) {
   State &s = S();
   std::lock_guard<std::mutex> lk(s.mu);
-  if (s.stream && s.device == device) return LK_OK;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(LK_ERR_DEVICE, "no HIP device visible");
-  if (device < 0 || device >= n) return fail(LK_ERR_INVALID_ARG, "device %d out of range (%d devices)", device, n);
-  HIP_TRY(hipSetDevice(device));
-  if (s.stream) HIP_TRY(hipStreamDestroy(s.stream));
-  HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  if (device < 0 || device >= n || device >= kMaxDevices)
+    return fail(LK_ERR_INVALID_ARG, "device %d out of range (%d devices)", device, n);
+  int rc = init_dev(device);
+  if (rc) return rc;
   s.device = device;
   return LK_OK;
 }
 
 void lk_weights_evict_all(void) {
-  State &s = S();
-  for (auto &kv : s.weights) (void)hipFree(kv.second);
-  s.weights.clear();
-  s.weight_bytes = 0;
+  for (auto &v : S().devs) {
+    for (auto &kv : v.weights) (void)hipFree(kv.second);
+    v.weights.clear();
+    v.weight_bytes = 0;
+  }
 }
 
-uint64_t lk_weights_cached_bytes(void) { return S().weight_bytes; }
+uint64_t lk_weights_cached_bytes(void) {
+  uint64_t t = 0;
+  for (auto &v : S().devs) t += v.weight_bytes;
+  return t;
+}
 
 void lk_shutdown(void) {
   State &s = S();
-  if (!s.stream) return;
-  (void)hipStreamSynchronize(s.stream);
-  lk_weights_evict_all();
-  for (int i = 0; i < 3; i++) {
-    if (s.scratch[i]) (void)hipFree(s.scratch[i]);
-    s.scratch[i] = nullptr;
-    s.scratch_bytes[i] = 0;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (int d = 0; d < kMaxDevices; d++) {
+    Dev &v = s.devs[d];
+    if (!v.stream) continue;
+    (void)hipSetDevice(d);
+    (void)hipStreamSynchronize(v.stream);
+    for (int i = 0; i < 3; i++) {
+      if (v.scratch[i]) (void)hipFree(v.scratch[i]);
+      v.scratch[i] = nullptr;
+      v.scratch_bytes[i] = 0;
+    }
+    (void)hipStreamDestroy(v.stream);
+    v.stream = nullptr;
   }
-  (void)hipStreamDestroy(s.stream);
-  s.stream = nullptr;
+  lk_weights_evict_all();
+  (void)hipSetDevice(prev);
   s.device = -1;
 }
 
@@ -615,15 +662,7 @@ int lk_weights_pin(const lk_tensor *a, uint64_t generation) {
   if (is_q(a->type)) bytes = (uint64_t)(t_num_elements(a) / 32) * block_bytes(a->type);
   else bytes = (uint64_t)t_num_elements(a) * (a->type == LK_TYPE_F16 ? 2 : 4);
   if (a->data_offset + bytes > a->buf_bytes) return fail(LK_ERR_OUT_OF_BOUNDS, "pin: tensor exceeds its buffer");
-  State &s = S();
-  auto key = std::make_tuple((uintptr_t)a->data, a->data_offset, bytes, generation);
-  if (s.weights.count(key)) return LK_OK;
-  void *dev = nullptr;
-  HIP_TRY(hipMalloc(&dev, std::max<uint64_t>(bytes, 4)));
-  HIP_TRY(hipMemcpy(dev, (const uint8_t *)a->data + a->data_offset, bytes, hipMemcpyHostToDevice));
-  s.weights[key] = dev;
-  s.weight_bytes += bytes;
-  return LK_OK;
+  return pin_on(cur(), a, a->data_offset, bytes, generation);
 }
 
 // Host-buffer operator: the Kotlin drop-in. ByteArrays stay authoritative; A comes
@@ -636,26 +675,18 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   if (c.empty) return LK_OK;
   rc = ensure_init();
   if (rc) return rc;
-  State &s = S();
+  Dev &s = cur();
   hipStream_t st = s.stream;
   const uint64_t a_bytes = c.a_hi - c.a_lo, b_bytes = c.b_hi - c.b_lo, d_bytes = c.d_hi - c.d_lo;
   // A: cached mirror or staged copy
-  const void *a_dev = nullptr;
-  for (auto &kv : s.weights) {
-    auto [base, off, bytes, gen] = kv.first;
-    (void)gen;
-    if (base == (uintptr_t)a->data && off <= c.a_lo && c.a_hi <= off + bytes) {
-      a_dev = (const uint8_t *)kv.second + (c.a_lo - off);
-      break;
-    }
-  }
+  const void *a_dev = find_pinned(s, a->data, c.a_lo, c.a_hi);
   if (!a_dev && a_bytes) {
-    if ((rc = ensure_scratch(0, a_bytes))) return rc;
+    if ((rc = ensure_scratch(s, 0, a_bytes))) return rc;
     HIP_TRY(hipMemcpyAsync(s.scratch[0], (const uint8_t *)a->data + c.a_lo, a_bytes, hipMemcpyHostToDevice, st));
     a_dev = s.scratch[0];
   }
-  if ((rc = ensure_scratch(1, std::max<uint64_t>(b_bytes, 16)))) return rc;
-  if ((rc = ensure_scratch(2, d_bytes))) return rc;
+  if ((rc = ensure_scratch(s, 1, std::max<uint64_t>(b_bytes, 16)))) return rc;
+  if ((rc = ensure_scratch(s, 2, d_bytes))) return rc;
   if (b_bytes) HIP_TRY(hipMemcpyAsync(s.scratch[1], (const uint8_t *)b->data + c.b_lo, b_bytes, hipMemcpyHostToDevice, st));
   // strided dst: preserve the bytes between written elements
   HIP_TRY(hipMemcpyAsync(s.scratch[2], (const uint8_t *)dst->data + c.d_lo, d_bytes, hipMemcpyHostToDevice, st));
@@ -670,6 +701,153 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   HIP_TRY(hipMemcpyAsync((uint8_t *)dst->data + c.d_lo, s.scratch[2], d_bytes, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   return LK_OK;
+}
+
+// ---- row-sharded host operator: one process, several GPUs (SURVEY §8b lk_mul_mat_sharded) -----
+//
+// Shard r owns rows [r·⌈M/P⌉, …) of A (whole blocks: contiguous bytes) and the same rows
+// of dst (ggml_hip/sharded.py shard_rows). Shard r runs on device r mod (visible devices),
+// so P may exceed the device count (shards on one device run back to back on its stream).
+// No collective: each shard writes its own disjoint rows of the host dst (D2H), which is
+// the all-gather of the in-process case. Work is issued on every device before any result
+// is read back, so the kernels of different devices overlap.
+
+namespace {
+
+void shard_span(int64_t M, int P, int r, int64_t *r0, int64_t *r1) {
+  const int64_t per = (M + P - 1) / P;
+  *r0 = std::min<int64_t>((int64_t)r * per, M);
+  *r1 = std::min<int64_t>(*r0 + per, M);
+}
+
+// Row pitch of A in bytes when rows can be cut as byte ranges, else 0.
+uint64_t a_row_pitch(const lk_tensor *a) {
+  if (is_q(a->type)) return a->ne[0] % 32 ? 0 : (uint64_t)(a->ne[0] / 32) * block_bytes(a->type);
+  return a->nb[1];
+}
+
+struct Shard {
+  int dev;
+  lk_tensor a, d;
+  Checked c;
+  const void *a_dev;
+  uint64_t a_stage_off, d_off;
+};
+
+}  // namespace
+
+int lk_weights_pin_sharded(const lk_tensor *a, uint64_t generation, int n_shards) {
+  if (!a || !a->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(LK_ERR_DEVICE, "no HIP device visible");
+  if (n_shards < 1) return fail(LK_ERR_INVALID_ARG, "n_shards %d", n_shards);
+  const uint64_t pitch = a_row_pitch(a);
+  if (!pitch || !is_q(a->type)) return fail(LK_ERR_NOT_IMPLEMENTED, "pin_sharded: quantized A with K %% 32 == 0 only");
+  if (a->data_offset + (uint64_t)a->ne[1] * pitch > a->buf_bytes)
+    return fail(LK_ERR_OUT_OF_BOUNDS, "pin: tensor exceeds its buffer");
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  int rc = LK_OK;
+  for (int r = 0; r < n_shards && rc == LK_OK; r++) {
+    int64_t r0, r1;
+    shard_span(a->ne[1], n_shards, r, &r0, &r1);
+    if (r1 <= r0) continue;
+    const int d = r % std::min(ndev, kMaxDevices);
+    if ((rc = init_dev(d))) break;
+    rc = pin_on(S().devs[d], a, a->data_offset + (uint64_t)r0 * pitch, (uint64_t)(r1 - r0) * pitch, generation);
+  }
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, int n_shards) {
+  Checked c;
+  int rc = check(a, b, dst, &c);
+  if (rc) return rc;
+  if (n_shards < 1) return fail(LK_ERR_INVALID_ARG, "n_shards %d", n_shards);
+  if (c.empty) return LK_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(LK_ERR_DEVICE, "no HIP device visible");
+  ndev = std::min(ndev, kMaxDevices);
+  // Rows must be byte ranges of A, and dst rows must not interleave (each shard copies
+  // its dst span back whole): otherwise one device computes everything.
+  const uint64_t pitch = a_row_pitch(a);
+  const uint64_t ew = dst->type == LK_TYPE_F16 ? 2 : 4;
+  const bool rows_ok = pitch && (uint64_t)(c.N - 1) * dst->nb[0] + ew <= dst->nb[1];
+  const int P = rows_ok ? (int)std::min<int64_t>(n_shards, c.M) : 1;
+  if (P == 1) return lk_mul_mat(a, b, dst);
+
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  std::vector<Shard> sh;
+  for (int r = 0; r < P; r++) {
+    int64_t r0, r1;
+    shard_span(c.M, P, r, &r0, &r1);
+    if (r1 <= r0) continue;
+    Shard x{};
+    x.dev = r % ndev;
+    x.a = *a; x.a.ne[1] = r1 - r0; x.a.data_offset = a->data_offset + (uint64_t)r0 * pitch;
+    x.d = *dst; x.d.ne[1] = r1 - r0; x.d.data_offset = dst->data_offset + (uint64_t)r0 * dst->nb[1];
+    if ((rc = check(&x.a, b, &x.d, &x.c))) return rc;
+    sh.push_back(x);
+  }
+  // per device: B once, A from the pin cache or staged, one dst span per shard
+  const uint64_t b_bytes = c.b_hi - c.b_lo;
+  std::vector<uint64_t> a_need(ndev, 0), d_need(ndev, 0);
+  std::vector<char> used(ndev, 0);
+  for (auto &x : sh) {
+    if ((rc = init_dev(x.dev))) goto out;
+    Dev &v = S().devs[x.dev];
+    used[x.dev] = 1;
+    x.a_dev = find_pinned(v, a->data, x.c.a_lo, x.c.a_hi);
+    x.a_stage_off = a_need[x.dev];
+    if (!x.a_dev) a_need[x.dev] += (x.c.a_hi - x.c.a_lo + 255) & ~255ull;
+    x.d_off = d_need[x.dev];
+    d_need[x.dev] += (x.c.d_hi - x.c.d_lo + 255) & ~255ull;
+  }
+  for (int d = 0; d < ndev; d++) {
+    if (!used[d]) continue;
+    Dev &v = S().devs[d];
+    if ((rc = init_dev(d))) goto out;
+    if ((rc = ensure_scratch(v, 0, std::max<uint64_t>(a_need[d], 16)))) goto out;
+    if ((rc = ensure_scratch(v, 1, std::max<uint64_t>(b_bytes, 16)))) goto out;
+    if ((rc = ensure_scratch(v, 2, std::max<uint64_t>(d_need[d], 16)))) goto out;
+    if (b_bytes && hipMemcpyAsync(v.scratch[1], (const uint8_t *)b->data + c.b_lo, b_bytes, hipMemcpyHostToDevice,
+                                  v.stream) != hipSuccess) { rc = fail(LK_ERR_DEVICE, "sharded: B upload"); goto out; }
+  }
+  for (auto &x : sh) {
+    Dev &v = S().devs[x.dev];
+    if ((rc = init_dev(x.dev))) goto out;
+    const uint64_t ab = x.c.a_hi - x.c.a_lo, db = x.c.d_hi - x.c.d_lo;
+    const void *a_dev = x.a_dev;
+    if (!a_dev) {
+      a_dev = (uint8_t *)v.scratch[0] + x.a_stage_off;
+      if (hipMemcpyAsync((void *)a_dev, (const uint8_t *)a->data + x.c.a_lo, ab, hipMemcpyHostToDevice, v.stream) !=
+          hipSuccess) { rc = fail(LK_ERR_DEVICE, "sharded: A upload"); goto out; }
+    }
+    void *d_dev = (uint8_t *)v.scratch[2] + x.d_off;
+    if (hipMemcpyAsync(d_dev, (const uint8_t *)dst->data + x.c.d_lo, db, hipMemcpyHostToDevice, v.stream) !=
+        hipSuccess) { rc = fail(LK_ERR_DEVICE, "sharded: dst upload"); goto out; }
+    lk_tensor da = x.a, dbt = *b, dd = x.d;
+    da.data = const_cast<void *>(a_dev); da.data_offset = 0; da.buf_bytes = ab;
+    dbt.data = v.scratch[1]; dbt.data_offset = 0; dbt.buf_bytes = b_bytes;
+    dd.data = d_dev; dd.data_offset = 0; dd.buf_bytes = db;
+    Checked cd = x.c;
+    cd.a_lo = 0; cd.a_hi = ab; cd.b_lo = 0; cd.b_hi = b_bytes; cd.d_lo = 0; cd.d_hi = db;
+    if ((rc = mul_mat_device_checked(&da, &dbt, &dd, cd, v.stream))) goto out;
+  }
+  for (auto &x : sh) {  // read back in issue order: every device's kernels are in flight
+    Dev &v = S().devs[x.dev];
+    if ((rc = init_dev(x.dev))) goto out;
+    if (hipMemcpyAsync((uint8_t *)dst->data + x.c.d_lo, (uint8_t *)v.scratch[2] + x.d_off, x.c.d_hi - x.c.d_lo,
+                       hipMemcpyDeviceToHost, v.stream) != hipSuccess) { rc = fail(LK_ERR_DEVICE, "sharded: dst read"); goto out; }
+  }
+  for (int d = 0; d < ndev; d++)
+    if (used[d] && hipStreamSynchronize(S().devs[d].stream) != hipSuccess && rc == LK_OK)
+      rc = fail(LK_ERR_DEVICE, "sharded: device %d failed", d);
+out:
+  (void)hipSetDevice(prev);
+  return rc;
 }
 
 // ---- plans: independent MUL_MAT nodes, one launch per quant type ---------------------------

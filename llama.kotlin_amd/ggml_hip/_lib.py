@@ -73,7 +73,7 @@ def raise_for_status(status: int, msg: str):
 
 EXPORTED_SYMBOLS = (
     "lk_init", "lk_device_count", "lk_last_error", "lk_shutdown", "lk_version",
-    "lk_mul_mat_validate", "lk_mul_mat", "lk_mul_mat_device",
+    "lk_mul_mat_validate", "lk_mul_mat", "lk_mul_mat_device", "lk_mul_mat_sharded", "lk_weights_pin_sharded",
     "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy",
     "lk_weights_pin", "lk_weights_evict_all", "lk_weights_cached_bytes",
     "lk_dequantize_device", "lk_quantize_device",
@@ -112,6 +112,8 @@ def load():
     L.lk_mul_mat_validate.argtypes = [P, P, P]
     L.lk_mul_mat.argtypes = [P, P, P]
     L.lk_mul_mat_device.argtypes = [P, P, P, vp]
+    L.lk_mul_mat_sharded.argtypes = [P, P, P, ctypes.c_int]
+    L.lk_weights_pin_sharded.argtypes = [P, ctypes.c_uint64, ctypes.c_int]
     L.lk_plan_create.argtypes = [P, P, P, ctypes.c_int, ctypes.POINTER(vp)]
     L.lk_plan_launch.argtypes = [vp, vp]
     L.lk_plan_num_launches.argtypes = [vp]

@@ -97,6 +97,17 @@ def computeMatMul(graphAllocator: GGMLGraphAllocator, context: GGMLContext | Non
     _lib.check(st)
 
 
+def computeMatMulSharded(graphAllocator: GGMLGraphAllocator, context: GGMLContext | None, a: GGMLTensor,
+                         b: GGMLTensor, dst: GGMLTensor, nShards: int) -> None:
+    """computeMatMul over host buffers with A's rows split over nShards GPUs of this process
+    (lk_mul_mat_sharded; shard r on device r mod device count). Same results as computeMatMul."""
+    if not all(_is_host(graphAllocator, t) for t in (a, b, dst)):
+        raise _lib.IllegalArgumentException("computeMatMulSharded takes host (ByteArray) buffers")
+    L = _lib.load()
+    la, lb, ld = to_lk(graphAllocator, a), to_lk(graphAllocator, b), to_lk(graphAllocator, dst)
+    _lib.check(L.lk_mul_mat_sharded(ctypes.byref(la), ctypes.byref(lb), ctypes.byref(ld), int(nShards)))
+
+
 def validateMatMul(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, b: GGMLTensor, dst: GGMLTensor) -> int:
     """computeMatMul's checks only; returns the lk_status code (0 = would run)."""
     L = _lib.load()
@@ -175,9 +186,14 @@ def weightsPin(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, generation: in
     _lib.check(_lib.load().lk_weights_pin(ctypes.byref(to_lk(graphAllocator, a)), generation))
 
 
+def weightsPinSharded(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, nShards: int, generation: int = 0):
+    """Pin each row shard of a on the device computeMatMulSharded runs it on."""
+    _lib.check(_lib.load().lk_weights_pin_sharded(ctypes.byref(to_lk(graphAllocator, a)), generation, int(nShards)))
+
+
 def weightsEvictAll():
     _lib.load().lk_weights_evict_all()
 
 
-__all__ = ["computeMatMul", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+__all__ = ["computeMatMul", "computeMatMulSharded", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
            "weightsEvictAll", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]

@@ -54,7 +54,8 @@ private fun fill(t: lk_tensor, src: GGMLTensor, base: CPointer<ByteVar>?, bytes:
  * (ByteArray, offset, size, generation) by lk_weights_pin; activations and dst are copied per call.
  */
 fun computeMatMulHip(graphAllocator: GGMLGraphAllocator, @Suppress("unused") context: GGMLContext,
-                     a: GGMLTensor, b: GGMLTensor, dst: GGMLTensor, weightGeneration: ULong = 0u) {
+                     a: GGMLTensor, b: GGMLTensor, dst: GGMLTensor, weightGeneration: ULong = 0u,
+                     shards: Int = 1) {
     val bufA = graphAllocator.buffers.getOrNull(a.bufferId)
     val bufB = graphAllocator.buffers.getOrNull(b.bufferId)
     val bufD = graphAllocator.buffers.getOrNull(dst.bufferId)
@@ -69,10 +70,15 @@ fun computeMatMulHip(graphAllocator: GGMLGraphAllocator, @Suppress("unused") con
                     fill(la, a, if (bufA != null && bufA.isNotEmpty()) pa.addressOf(0) else null, bufA?.size ?: 0)
                     fill(lb, b, if (bufB != null && bufB.isNotEmpty()) pb.addressOf(0) else null, bufB?.size ?: 0)
                     fill(ld, dst, if (bufD != null && bufD.isNotEmpty()) pd.addressOf(0) else null, bufD?.size ?: 0)
-                    if (a.type == GGMLType.Q4_0 || a.type == GGMLType.Q4_1 || a.type == GGMLType.Q8_0) {
-                        checkStatus(lk_weights_pin(la.ptr, weightGeneration))
+                    val quant = a.type == GGMLType.Q4_0 || a.type == GGMLType.Q4_1 || a.type == GGMLType.Q8_0
+                    if (shards > 1) {
+                        // rows of A over the node's GPUs (shard r on device r mod lk_device_count())
+                        if (quant && a.ne[0] % 32L == 0L) checkStatus(lk_weights_pin_sharded(la.ptr, weightGeneration, shards))
+                        checkStatus(lk_mul_mat_sharded(la.ptr, lb.ptr, ld.ptr, shards))
+                    } else {
+                        if (quant) checkStatus(lk_weights_pin(la.ptr, weightGeneration))
+                        checkStatus(lk_mul_mat(la.ptr, lb.ptr, ld.ptr))
                     }
-                    checkStatus(lk_mul_mat(la.ptr, lb.ptr, ld.ptr))
                 }
             }
         }
@@ -80,7 +86,7 @@ fun computeMatMulHip(graphAllocator: GGMLGraphAllocator, @Suppress("unused") con
 }
 
 /** A GGMLBackend that offloads MUL_MAT to the MI355X and defers everything else to the CPU backend. */
-class GGMLHipBackend(private val device: Int = 0) : GGMLBackend {
+class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) : GGMLBackend {
     private val cpu = GGMLCpuBackend()
 
     init {
@@ -111,7 +117,7 @@ class GGMLHipBackend(private val device: Int = 0) : GGMLBackend {
             for (i in 0 until graph.nNodes) {
                 val node = graph.nodes[i] ?: continue
                 if (supportsOp(node)) {
-                    computeMatMulHip(ga, ga.context, node.src[0]!!, node.src[1]!!, node)
+                    computeMatMulHip(ga, ga.context, node.src[0]!!, node.src[1]!!, node, shards = shards)
                 } else {
                     // one-node graph on the CPU backend (K/core/GGMLCpuBackend.kt:167-176)
                     val one = GGMLCGraph(size = 1, nNodes = 1, nodes = arrayOf(node), allocator = ga)

@@ -36,8 +36,10 @@ def noise_for(O, qt, q, M, K, x):
     return acc_noise(w, np.abs(x), split=x.shape[1] > 1)
 
 
-def gpu_matmul(qt, q, M, K, N, x, a_off=0, b_off=0, d_off=0, dst_row_pad=0, b_stride=None, host=False):
-    """Run computeMatMul through the ggml_hip mirror; returns dst as [M, N] float32."""
+def gpu_matmul(qt, q, M, K, N, x, a_off=0, b_off=0, d_off=0, dst_row_pad=0, b_stride=None, host=False,
+               n_shards=0, pin=False):
+    """Run computeMatMul through the ggml_hip mirror; returns dst as [M, N] float32.
+    n_shards > 0: computeMatMulSharded over host buffers (pin: weightsPinSharded first)."""
     import ggml_hip as G
     ga = G.GGMLGraphAllocator(device="host" if host else "cuda", defaultBufferSize=16)
     a_bytes = q.size
@@ -57,7 +59,12 @@ def gpu_matmul(qt, q, M, K, N, x, a_off=0, b_off=0, d_off=0, dst_row_pad=0, b_st
     xb = np.zeros((K, bcol), np.float32)
     xb[:, :N] = x
     ga.setTensorBytes(b, xb.view(np.uint8).reshape(-1))
-    G.computeMatMul(ga, ga.context, a, b, d)
+    if n_shards:
+        if pin:
+            G.weightsPinSharded(ga, a, n_shards)
+        G.computeMatMulSharded(ga, ga.context, a, b, d, n_shards)
+    else:
+        G.computeMatMul(ga, ga.context, a, b, d)
     raw = ga.buffers[idd]
     raw = raw if isinstance(raw, np.ndarray) else raw.cpu().numpy()
     out = raw[d_off:d_off + d_bytes].view(np.float32).reshape(M, d_row)[:, :N]
