@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--no-chain", action="store_true")
     ap.add_argument("--no-batched", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=6144)
     args = ap.parse_args()
 
@@ -236,6 +237,8 @@ def main():
         result["headline_q4_0_4096x4096_n1"] = headline(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_batched:
         result["batched"] = batched(torch, G, dev)
+    if rank == 0 and world == 1 and not args.no_host_path:
+        result["host_path_pcie"] = host_path(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, token_bytes)
     if rank == 0:
@@ -419,6 +422,70 @@ def batched(torch, G, dev, reps=10):
                      "rotating_weight_copies": copies, "hip_graph": gr is not None}
         del g
     return out
+
+
+def host_path(torch, G, dev, layers=LAYERS, reps=5):
+    """The Kotlin drop-in case, PCIe included (never `value`): Llama-7B layers on HOST buffers
+    (ByteArray-backed), weights pinned on the device once. Per layer the dependent schedule
+    {q,k,v} -> o -> {gate,up} -> down. Three ways to run it:
+      per_node  — one lk_mul_mat per node (what computeMatMulHip does): B up, dst down, sync;
+      graph_all — one ResidentGraph over all nodes, every dst written back (same semantics);
+      graph_out — the same graph writing back only each layer's down output.
+    Reported per token (x 32 / `layers`; all 32 layers by default, 3.65 GB of host weights)."""
+    import numpy as np
+    T = G.GGMLType
+    total = layers * sum(alg_bytes(M, K) + 64 for (_, M, K) in LAYER_MATS) + 4 * HIDDEN + 64
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=total)  # one ByteArray, no regrowth
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    nodes, outs = [], []
+    x = ga.allocateTensor(T.F32, [1, HIDDEN], bufferId=0)
+    ga.setTensorBytes(x, np.random.default_rng(1).standard_normal(HIDDEN).astype(np.float32))
+    act = {"h": x}
+    for _ in range(layers):
+        for grp in CHAIN:
+            for name in grp:
+                M, K = next((m, k) for (n, m, k) in LAYER_MATS if n == name)
+                src = act[X_OF[name]]
+                a = ga.allocateTensor(T.Q4_0, [K, M])
+                w = torch.randn(M * K, generator=gen, device=dev) * 0.02
+                ga.setTensorBytes(a, G.quantizeTensor(w, T.Q4_0).cpu().numpy())
+                del w
+                d = ga.allocateTensor(T.F32, [1, M])
+                nodes.append((a, src, d))
+                outs.append(name == "down")
+                if name in ("q", "o", "up", "down"):  # {q,k,v} -> o -> {gate,up} -> down -> next layer
+                    act[{"q": "attn", "o": "h2", "up": "ffn", "down": "h"}[name]] = d
+    for a, _, _ in nodes:
+        G.weightsPin(ga, a)
+    lay = 32 / layers
+
+    def per_node():
+        for a, b, d in nodes:
+            G.computeMatMul(ga, ga.context, a, b, d)
+
+    res = {"layers_timed": layers, "weights_pinned": True}
+    for key, fn in (("per_node", per_node),):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        per = (time.perf_counter() - t0) / reps * lay
+        res[key] = {"ms_per_token": round(per * 1e3, 3), "tokens_per_s": round(1 / per, 2)}
+    for key, mask in (("graph_all", None), ("graph_out", outs)):
+        g = G.ResidentGraph(ga, nodes, outputs=mask)
+        g.compute()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            g.compute()
+        per = (time.perf_counter() - t0) / reps * lay
+        res[key] = {"ms_per_token": round(per * 1e3, 3), "tokens_per_s": round(1 / per, 2),
+                    "launches_per_layer": g.numLaunches / layers,
+                    "h2d_bytes_per_token": int(g.transferBytes(True) * lay),
+                    "d2h_bytes_per_token": int(g.transferBytes(False) * lay)}
+        g.close()
+    G.weightsEvictAll()
+    return res
 
 
 def cpu_baseline(sample_rows, token_bytes):

@@ -25,6 +25,8 @@
  *   lk_mul_mat_sharded    SURVEY §8b's sharded entry: computeMatMul with A's rows split
  *                         over the GPUs of one node from one host thread (the reference
  *                         is single-device; this is the north star's row sharding).
+ *   lk_graph_*            core/GGMLComputeOps.kt:2515-2652 computeGraph/computeMulMat over
+ *                         host buffers with activations kept in HBM between nodes.
  *   lk_weights_pin/evict  residency cache behind GGMLBackendBuffer.setTensor
  *                         (core/GGMLBackend.kt:63-69) for host-authoritative ByteArrays.
  *   lk_dequantize_device  core/GGMLComputeOps.kt:918 dequantizeTensor (Q8_0/Q4_0/Q4_1).
@@ -160,6 +162,26 @@ int lk_plan_launch(lk_plan *plan, void *stream);
 /* Number of kernel launches one lk_plan_launch issues. */
 int lk_plan_num_launches(const lk_plan *plan);
 void lk_plan_destroy(lk_plan *plan);
+
+/* ---- graph residency over host buffers ---------------------------------------
+ * GGMLComputeOps.computeGraph / computeMulMat (core/GGMLComputeOps.kt:2515-2652) for a
+ * graph of n MUL_MAT nodes on host ByteArrays, kept device-resident between nodes
+ * (SURVEY §8f row 2). Nodes are given in graph order; a node that reads bytes an earlier
+ * node writes runs after it. Quantized A operands no node writes are weights: pinned once
+ * (keyed with weight_generation). Every other range gets a device mirror; a compute
+ * uploads only ranges no earlier node produces, runs each dependency level as one
+ * lk_plan, and writes back the dst of nodes with outputs[i] != 0 (outputs = NULL: all).
+ * Same results as n lk_mul_mat calls in order. */
+typedef struct lk_graph lk_graph;
+int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
+                    const uint8_t *outputs, uint64_t weight_generation, lk_graph **out);
+/* Upload inputs, run, write outputs back; synchronous. */
+int lk_graph_compute(lk_graph *g);
+int lk_graph_num_levels(const lk_graph *g);
+int lk_graph_num_launches(const lk_graph *g);
+/* Bytes one lk_graph_compute moves host->device (to_device = 1) or back (0). */
+uint64_t lk_graph_transfer_bytes(const lk_graph *g, int to_device);
+void lk_graph_destroy(lk_graph *g);
 
 /* ---- weight residency (host path) ------------------------------------------ */
 

@@ -1040,3 +1040,250 @@ int lk_repack_q4_device(void *blocks, int64_t n_blocks, int32_t type, int32_t di
 }
 
 }  // extern "C"
+
+// ---- graph residency over host buffers ----------------------------------
+//
+// A sequence of MUL_MAT nodes over host ByteArrays, analysed once: quantized weights are
+// pinned on the device, every activation byte range (B operands, F32/F16 A operands, dst)
+// gets one device mirror, nodes are levelled by their read/write overlaps, and each level
+// becomes one lk_plan. A compute uploads only the graph's inputs (ranges no earlier node
+// produces, plus strided dst ranges whose gap bytes must survive), runs the levels
+// back to back on the device, and writes back the dst ranges of the output nodes.
+// Intermediate activations never cross PCIe.
+
+struct lk_graph {
+  struct Region { uintptr_t host; uint64_t lo, hi; uint8_t *dev; void *alloc; };
+  struct Copy { uint8_t *host; uint8_t *dev; uint64_t bytes; uint64_t stage; };
+  int device = 0;
+  std::vector<Region> regions;
+  std::vector<lk_plan *> levels;
+  std::vector<Copy> h2d, d2h;
+  std::vector<int> node_level;
+  uint8_t *staging = nullptr;  // page-locked bounce buffer for the per-compute copies
+  int computes = 0;             // the second compute captures the device part in a HIP graph
+  bool no_capture = false;
+  hipGraphExec_t exec = nullptr;
+  uint64_t h2d_bytes = 0, d2h_bytes = 0;
+};
+
+namespace {
+
+struct Span {
+  uintptr_t host;
+  uint64_t lo, hi;
+};
+bool overlaps(const Span &x, const Span &y) { return x.host == y.host && x.lo < y.hi && y.lo < x.hi; }
+
+// Union of spans per host buffer, as sorted disjoint intervals.
+std::vector<Span> merge_spans(std::vector<Span> v) {
+  std::sort(v.begin(), v.end(), [](const Span &x, const Span &y) {
+    return x.host != y.host ? x.host < y.host : x.lo < y.lo;
+  });
+  std::vector<Span> out;
+  for (auto &s : v) {
+    if (s.hi <= s.lo) continue;
+    if (!out.empty() && out.back().host == s.host && s.lo <= out.back().hi) out.back().hi = std::max(out.back().hi, s.hi);
+    else out.push_back(s);
+  }
+  return out;
+}
+
+uint8_t *mirror_of(lk_graph *g, uintptr_t host, uint64_t lo) {
+  for (auto &r : g->regions)
+    if (r.host == host && r.lo <= lo && lo < r.hi) return r.dev + (lo - r.lo);
+  for (auto &r : g->regions)  // empty span at a region end
+    if (r.host == host && r.lo <= lo && lo <= r.hi) return r.dev + (lo - r.lo);
+  return nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+void lk_graph_destroy(lk_graph *g) {
+  if (!g) return;
+  for (auto *p : g->levels) lk_plan_destroy(p);
+  for (auto &r : g->regions) (void)hipFree(r.alloc);
+  if (g->staging) (void)hipHostFree(g->staging);
+  if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  delete g;
+}
+
+int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n, const uint8_t *outputs,
+                    uint64_t weight_generation, lk_graph **out) {
+  if (!out || n < 0 || (n && (!a || !b || !dst))) return fail(LK_ERR_INVALID_ARG, "bad graph arguments");
+  *out = nullptr;
+  int rc = ensure_init();
+  if (rc) return rc;
+  Dev &v = cur();
+  std::vector<Checked> c(n);
+  std::vector<char> a_weight(n, 0);
+  std::vector<Span> dsp(n), asp(n), bsp(n);
+  for (int i = 0; i < n; i++) {
+    if ((rc = check(&a[i], &b[i], &dst[i], &c[i]))) return rc;
+    asp[i] = {(uintptr_t)a[i].data, c[i].a_lo, c[i].a_hi};
+    bsp[i] = {(uintptr_t)b[i].data, c[i].b_lo, c[i].b_hi};
+    dsp[i] = {(uintptr_t)dst[i].data, c[i].d_lo, c[i].d_hi};
+  }
+  // quantized A that no node writes: a weight (pinned); anything else is an activation
+  for (int i = 0; i < n; i++) {
+    bool produced = false;
+    for (int j = 0; j < n && !produced; j++) produced = overlaps(asp[i], dsp[j]);
+    a_weight[i] = is_q(a[i].type) && !produced && !c[i].empty;
+  }
+  auto g = new lk_graph();
+  g->device = S().device;
+  g->node_level.assign(n, 0);
+  int nlev = 0;
+  for (int j = 0; j < n; j++) {  // level = 1 + deepest earlier node it conflicts with
+    int lev = 0;
+    for (int i = 0; i < j; i++) {
+      const bool raw = overlaps(dsp[i], bsp[j]) || overlaps(dsp[i], asp[j]);
+      const bool war = overlaps(bsp[i], dsp[j]) || overlaps(asp[i], dsp[j]);
+      const bool waw = overlaps(dsp[i], dsp[j]);
+      if (raw || war || waw) lev = std::max(lev, g->node_level[i] + 1);
+    }
+    g->node_level[j] = lev;
+    nlev = std::max(nlev, lev + 1);
+  }
+  // device mirrors of every activation range
+  std::vector<Span> act;
+  for (int i = 0; i < n; i++) {
+    if (c[i].empty) continue;
+    act.push_back(bsp[i]);
+    act.push_back(dsp[i]);
+    if (!a_weight[i]) act.push_back(asp[i]);
+  }
+  for (auto &s : merge_spans(act)) {
+    // the mirror keeps the host address modulo 256, so operands keep their alignment class
+    lk_graph::Region r{s.host, s.lo, s.hi, nullptr, nullptr};
+    const uint64_t skew = (s.host + s.lo) & 255;
+    if (hipMalloc(&r.alloc, s.hi - s.lo + skew) != hipSuccess) {
+      lk_graph_destroy(g);
+      return fail(LK_ERR_DEVICE, "graph: mirror allocation of %llu B", (unsigned long long)(s.hi - s.lo));
+    }
+    r.dev = (uint8_t *)r.alloc + skew;
+    g->regions.push_back(r);
+  }
+  // inputs: read ranges not produced by an earlier node, and non-dense dst ranges (their gap
+  // bytes are copied back whole); uploading all of them up front is safe because levels
+  // order every in-graph write after the reads that precede it
+  std::vector<Span> up, down;
+  for (int j = 0; j < n; j++) {
+    if (c[j].empty) continue;
+    auto produced_before = [&](const Span &s) {
+      for (int i = 0; i < j; i++) if (overlaps(dsp[i], s)) return true;
+      return false;
+    };
+    if (!produced_before(bsp[j])) up.push_back(bsp[j]);
+    if (!a_weight[j] && !produced_before(asp[j])) up.push_back(asp[j]);
+    const uint64_t ew = dst[j].type == LK_TYPE_F16 ? 2 : 4;
+    if (dsp[j].hi - dsp[j].lo != (uint64_t)c[j].M * c[j].N * ew) up.push_back(dsp[j]);
+    if (!outputs || outputs[j]) down.push_back(dsp[j]);
+  }
+  // a read range produced by an earlier node is not uploaded even in part: the producer writes it
+  for (auto &s : merge_spans(up)) {
+    g->h2d.push_back({(uint8_t *)s.host + s.lo, mirror_of(g, s.host, s.lo), s.hi - s.lo, 0});
+    g->h2d_bytes += s.hi - s.lo;
+  }
+  for (auto &s : merge_spans(down)) {
+    g->d2h.push_back({(uint8_t *)s.host + s.lo, mirror_of(g, s.host, s.lo), s.hi - s.lo, 0});
+    g->d2h_bytes += s.hi - s.lo;
+  }
+  // pinned staging for everything that crosses PCIe each compute: the host side of a copy
+  // is a CPU memcpy, the PCIe side a DMA from page-locked memory (pageable copies are staged
+  // by the runtime in small synchronous chunks). User memory is never page-locked: a
+  // registration covering part of a ByteArray breaks other copies that straddle its edge.
+  {
+    uint64_t off = 0;
+    for (auto &x : g->h2d) { x.stage = off; off += (x.bytes + 255) & ~255ull; }
+    for (auto &x : g->d2h) { x.stage = off; off += (x.bytes + 255) & ~255ull; }
+    if (off && hipHostMalloc((void **)&g->staging, off, hipHostMallocDefault) != hipSuccess) {
+      lk_graph_destroy(g);
+      return fail(LK_ERR_DEVICE, "graph: pinned staging of %llu B", (unsigned long long)off);
+    }
+  }
+  // weights, then one plan per level over device descriptors
+  std::vector<lk_tensor> da(n), db(n), dd(n);
+  for (int i = 0; i < n; i++) {
+    da[i] = a[i]; db[i] = b[i]; dd[i] = dst[i];
+    if (c[i].empty) continue;
+    if (a_weight[i]) {
+      const uint64_t bytes = c[i].a_hi - c[i].a_lo;
+      if ((rc = pin_on(v, &a[i], c[i].a_lo, bytes, weight_generation))) { lk_graph_destroy(g); return rc; }
+      const void *p = find_pinned(v, a[i].data, c[i].a_lo, c[i].a_hi);
+      da[i].data = (uint8_t *)p - c[i].a_lo;  // keep data_offset: base shifted so base + offset = mirror
+      da[i].buf_bytes = c[i].a_hi;
+    } else {
+      da[i].data = mirror_of(g, asp[i].host, c[i].a_lo) - c[i].a_lo;
+      da[i].buf_bytes = c[i].a_hi;
+    }
+    db[i].data = mirror_of(g, bsp[i].host, c[i].b_lo) - c[i].b_lo;
+    db[i].buf_bytes = c[i].b_hi;
+    dd[i].data = mirror_of(g, dsp[i].host, c[i].d_lo) - c[i].d_lo;
+    dd[i].buf_bytes = c[i].d_hi;
+  }
+  for (int l = 0; l < nlev; l++) {
+    std::vector<lk_tensor> la, lb, ld;
+    for (int i = 0; i < n; i++)
+      if (g->node_level[i] == l && !c[i].empty) { la.push_back(da[i]); lb.push_back(db[i]); ld.push_back(dd[i]); }
+    if (la.empty()) continue;
+    lk_plan *p = nullptr;
+    if ((rc = lk_plan_create(la.data(), lb.data(), ld.data(), (int)la.size(), &p))) { lk_graph_destroy(g); return rc; }
+    g->levels.push_back(p);
+  }
+  *out = g;
+  return LK_OK;
+}
+
+int lk_graph_compute(lk_graph *g) {
+  if (!g) return fail(LK_ERR_INVALID_ARG, "null graph");
+  int rc = lk_init(g->device);
+  if (rc) return rc;
+  hipStream_t st = cur().stream;
+  // device part: staged uploads, every level, staged write-backs — replayed as one HIP graph
+  // from the second compute on (the first one sizes any scratch the kernels grow)
+  auto enqueue = [&]() -> int {
+    for (auto &x : g->h2d) HIP_TRY(hipMemcpyAsync(x.dev, g->staging + x.stage, x.bytes, hipMemcpyHostToDevice, st));
+    for (auto *p : g->levels) {
+      int r = lk_plan_launch(p, st);
+      if (r) return r;
+    }
+    for (auto &x : g->d2h) HIP_TRY(hipMemcpyAsync(g->staging + x.stage, x.dev, x.bytes, hipMemcpyDeviceToHost, st));
+    return LK_OK;
+  };
+  for (auto &x : g->h2d) std::memcpy(g->staging + x.stage, x.host, x.bytes);
+  if (!g->exec && !g->no_capture && g->computes >= 1) {
+    hipGraph_t graph = nullptr;
+    bool ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    const int r = ok ? enqueue() : LK_ERR_DEVICE;
+    ok = (hipStreamEndCapture(st, &graph) == hipSuccess) && ok && r == LK_OK;
+    if (ok) ok = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0) == hipSuccess;
+    if (graph) (void)hipGraphDestroy(graph);
+    if (!ok) {
+      g->exec = nullptr;
+      g->no_capture = true;  // stay eager
+      (void)hipGetLastError();
+    }
+  }
+  if (g->exec) HIP_TRY(hipGraphLaunch(g->exec, st));
+  else if ((rc = enqueue())) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  for (auto &x : g->d2h) std::memcpy(x.host, g->staging + x.stage, x.bytes);
+  g->computes++;
+  return LK_OK;
+}
+
+int lk_graph_num_levels(const lk_graph *g) { return g ? (int)g->levels.size() : 0; }
+
+int lk_graph_num_launches(const lk_graph *g) {
+  int t = 0;
+  if (g) for (auto *p : g->levels) t += lk_plan_num_launches(p);
+  return t;
+}
+
+uint64_t lk_graph_transfer_bytes(const lk_graph *g, int to_device) {
+  return g ? (to_device ? g->h2d_bytes : g->d2h_bytes) : 0;
+}
+
+}  // extern "C"

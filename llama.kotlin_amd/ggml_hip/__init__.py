@@ -16,7 +16,7 @@ from . import _lib
 from ._lib import (HipDeviceError, IllegalArgumentException, IllegalStateException, IndexOutOfBoundsException,
                    NotOffloadedError)
 from .backend import GGMLBackendRegistry, GGMLHipBackend, GGMLStatus
-from .ops import (MulMatPlan, computeMatMul, computeMatMulSharded, dequantizeTensor, quantizeTensor, to_lk, validateMatMul, weightsEvictAll,
+from .ops import (MulMatPlan, ResidentGraph, computeMatMul, computeMatMulSharded, dequantizeTensor, quantizeTensor, to_lk, validateMatMul, weightsEvictAll,
                   weightsPin, weightsPinSharded)
 from .gguf import GGUFContext, GGUFParser, GGUFTensorInfo, GGUFType, LoadedModel, ModelLoader
 from .sharded import RowShardedMulMat, row_slice, shard_rows
@@ -26,7 +26,7 @@ from .tensor import (GGMLCGraph, GGMLContext, GGMLGraphAllocator, GGMLOp, GGMLTe
 __all__ = [
     "GGMLType", "GGMLTensor", "GGMLGraphAllocator", "GGMLContext", "GGMLCGraph", "GGMLOp",
     "calculateContiguousStrides", "calculateTensorByteSize",
-    "computeMatMul", "computeMatMulSharded", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+    "computeMatMul", "computeMatMulSharded", "weightsPinSharded", "validateMatMul", "MulMatPlan", "ResidentGraph", "dequantizeTensor", "quantizeTensor", "weightsPin",
     "weightsEvictAll", "to_lk",
     "GGMLHipBackend", "GGMLStatus", "GGMLBackendRegistry",
     "RowShardedMulMat", "row_slice", "shard_rows",

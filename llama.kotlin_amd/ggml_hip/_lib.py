@@ -75,6 +75,8 @@ EXPORTED_SYMBOLS = (
     "lk_init", "lk_device_count", "lk_last_error", "lk_shutdown", "lk_version",
     "lk_mul_mat_validate", "lk_mul_mat", "lk_mul_mat_device", "lk_mul_mat_sharded", "lk_weights_pin_sharded",
     "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy",
+    "lk_graph_create", "lk_graph_compute", "lk_graph_num_levels", "lk_graph_num_launches",
+    "lk_graph_transfer_bytes", "lk_graph_destroy",
     "lk_weights_pin", "lk_weights_evict_all", "lk_weights_cached_bytes",
     "lk_dequantize_device", "lk_quantize_device",
     # include/lk_gguf.h
@@ -119,6 +121,14 @@ def load():
     L.lk_plan_num_launches.argtypes = [vp]
     L.lk_plan_destroy.argtypes = [vp]
     L.lk_plan_destroy.restype = None
+    L.lk_graph_create.argtypes = [P, P, P, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(vp)]
+    L.lk_graph_compute.argtypes = [vp]
+    L.lk_graph_num_levels.argtypes = [vp]
+    L.lk_graph_num_launches.argtypes = [vp]
+    L.lk_graph_transfer_bytes.argtypes = [vp, ctypes.c_int]
+    L.lk_graph_transfer_bytes.restype = ctypes.c_uint64
+    L.lk_graph_destroy.argtypes = [vp]
+    L.lk_graph_destroy.restype = None
     L.lk_weights_pin.argtypes = [P, ctypes.c_uint64]
     L.lk_weights_evict_all.restype = None
     L.lk_weights_cached_bytes.restype = ctypes.c_uint64

@@ -17,7 +17,7 @@ from __future__ import annotations
 import enum
 
 from . import _lib
-from .ops import MulMatPlan, computeMatMul
+from .ops import MulMatPlan, ResidentGraph, _is_host, computeMatMul
 from .tensor import GGMLCGraph, GGMLOp, GGMLTensor, GGMLType
 
 
@@ -155,14 +155,27 @@ class GGMLHipBackend:
 
     def graphCompute(self, graph: GGMLCGraph) -> GGMLStatus:
         """Compute every MUL_MAT node of the graph (core/GGMLCpuBackend.kt:167-176 contract:
-        any operator exception -> FAILED). Nodes of one graph are taken as mutually
-        independent MUL_MATs (no node reads another's dst) and run as one plan."""
+        any operator exception -> FAILED).
+
+        Host (ByteArray) allocators: one ResidentGraph per node set, cached — weights pinned,
+        activations kept in HBM between dependent nodes, levels of independent nodes grouped.
+        Device allocators: mutually independent nodes run as one plan, otherwise in order."""
         ga = graph.allocator or self.graphAllocator
         try:
             nodes = [n for n in graph.nodes[: graph.nNodes] if n is not None and n.op != GGMLOp.NONE]
             for n in nodes:
                 if not self.supportsOp(n):
                     raise _lib.NotOffloadedError(f"node {n.name!r} ({n.op}) is not supported by the HIP backend")
+            if nodes and _is_host(ga, nodes[0]):
+                key = ("host",) + tuple((id(n), n.dataOffset, n.src[0].dataOffset, n.src[1].dataOffset,
+                                         ga.dataPtr(n.bufferId), ga.dataPtr(n.src[0].bufferId),
+                                         ga.dataPtr(n.src[1].bufferId)) for n in nodes)
+                g = self._plans.get(key)
+                if g is None:
+                    g = ResidentGraph(ga, [(n.src[0], n.src[1], n) for n in nodes])
+                    self._plans[key] = g
+                g.compute()
+                return GGMLStatus.SUCCESS
             ids = {id(n) for n in nodes}
             independent = all(id(s) not in ids for n in nodes for s in n.src[:2] if s is not None)
             if independent and len(nodes) > 1:

@@ -152,6 +152,55 @@ class MulMatPlan:
             pass
 
 
+class ResidentGraph:
+    """GGMLComputeOps.computeGraph over MUL_MAT nodes on HOST buffers (core/GGMLComputeOps.kt:
+    2515-2652) with the activations kept in HBM between nodes (lk_graph_*).
+
+    ``nodes``: [(a, b, dst)] in graph order; a node reading bytes an earlier node writes runs
+    after it. ``outputs``: per-node flags for which dst bytes are written back (None: all).
+    Quantized A operands no node writes are pinned once (``weightGeneration``)."""
+
+    def __init__(self, ga: GGMLGraphAllocator, nodes, outputs=None, weightGeneration: int = 0):
+        L = _lib.load()
+        n = len(nodes)
+        A = (_lib.LkTensor * max(n, 1))()
+        B = (_lib.LkTensor * max(n, 1))()
+        D = (_lib.LkTensor * max(n, 1))()
+        for i, (a, b, d) in enumerate(nodes):
+            A[i], B[i], D[i] = to_lk(ga, a), to_lk(ga, b), to_lk(ga, d)
+        outs = None
+        if outputs is not None:
+            outs = (ctypes.c_uint8 * max(n, 1))(*[1 if o else 0 for o in outputs])
+        self._handle = ctypes.c_void_p()
+        _lib.check(L.lk_graph_create(A, B, D, n, outs, weightGeneration, ctypes.byref(self._handle)))
+        self._keep = (ga, A, B, D, outs)
+
+    def compute(self):
+        _lib.check(_lib.load().lk_graph_compute(self._handle))
+
+    @property
+    def numLevels(self) -> int:
+        return _lib.load().lk_graph_num_levels(self._handle)
+
+    @property
+    def numLaunches(self) -> int:
+        return _lib.load().lk_graph_num_launches(self._handle)
+
+    def transferBytes(self, toDevice: bool) -> int:
+        return int(_lib.load().lk_graph_transfer_bytes(self._handle, 1 if toDevice else 0))
+
+    def close(self):
+        if self._handle:
+            _lib.load().lk_graph_destroy(self._handle)
+            self._handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def dequantizeTensor(graphAllocator: GGMLGraphAllocator, tensor: GGMLTensor, stream=None):
     """core/GGMLComputeOps.kt:918 for Q8_0/Q4_0/Q4_1 on device: returns a float32 torch tensor
     of numElements values (bit-exact with the reference)."""
@@ -195,5 +244,5 @@ def weightsEvictAll():
     _lib.load().lk_weights_evict_all()
 
 
-__all__ = ["computeMatMul", "computeMatMulSharded", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+__all__ = ["computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
            "weightsEvictAll", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]

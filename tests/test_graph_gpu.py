@@ -1,0 +1,148 @@
+"""Graph residency over host buffers (lk_graph_*): a MUL_MAT graph on
+ByteArray-backed tensors computed with the activations kept in HBM between nodes. Every
+result must equal the same nodes run one computeMatMul at a time (bit for bit: the same
+kernels compute each node), and only graph inputs may cross PCIe on the way in."""
+import numpy as np
+import pytest
+
+from _util import random_acts, random_weights
+
+pytestmark = pytest.mark.gpu
+
+
+def _layer(ga, oracle, K=256, F=384, N=1, seed=0):
+    """A Llama-style block on host buffers: q,k,v,gate,up from x; o from q; down from up."""
+    import ggml_hip as G
+    x = ga.allocateTensor(G.GGMLType.F32, [N, K], name="x")
+    ga.setTensorBytes(x, random_acts(K * N, seed + 1))
+    W, nodes = {}, []
+
+    def weight(name, qt, k, m, s):
+        t = ga.allocateTensor(G.GGMLType(qt), [k, m], name=name)
+        ga.setTensorBytes(t, oracle.quantize(qt, random_weights(k * m, s)))
+        W[name] = t
+        return t
+
+    def node(name, a, b, m):
+        d = ga.allocateTensor(G.GGMLType.F32, [N, m], name=name)
+        nodes.append((a, b, d))
+        return d
+
+    q = node("q", weight("wq", 2, K, K, seed + 2), x, K)
+    node("k", weight("wk", 3, K, K, seed + 3), x, K)
+    node("v", weight("wv", 6, K, K, seed + 4), x, K)
+    node("o", weight("wo", 2, K, K, seed + 5), q, K)
+    node("g", weight("wg", 2, K, F, seed + 6), x, F)
+    u = node("u", weight("wu", 2, K, F, seed + 7), x, F)
+    node("d", weight("wd", 2, F, K, seed + 8), u, K)
+    return x, nodes
+
+
+def _sequential(ga, nodes):
+    import ggml_hip as G
+    for a, b, d in nodes:
+        G.computeMatMul(ga, ga.context, a, b, d)
+    return [bytes(ga.tensorBytes(d)) for _, _, d in nodes]
+
+
+@pytest.mark.parametrize("N", [1, 4])
+def test_layer_graph_equals_sequential(gpu, oracle, N):
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 20)
+    x, nodes = _layer(ga, oracle, N=N)
+    want = _sequential(ga, nodes)
+    for _, _, d in nodes:
+        ga.setTensorBytes(d, np.zeros(4 * d.ne[0] * d.ne[1], np.uint8))
+    g = G.ResidentGraph(ga, nodes)
+    assert g.numLevels == 2
+    assert g.transferBytes(True) == 4 * N * 256  # only x goes up: weights pinned, q and u stay in HBM
+    assert g.transferBytes(False) == sum(4 * d.ne[0] * d.ne[1] for _, _, d in nodes)
+    g.compute()
+    assert [bytes(ga.tensorBytes(d)) for _, _, d in nodes] == want
+    # a new input is picked up by the next compute
+    ga.setTensorBytes(x, random_acts(256 * N, 99))
+    want2 = _sequential(ga, nodes)
+    g.compute()
+    assert [bytes(ga.tensorBytes(d)) for _, _, d in nodes] == want2
+
+
+def test_outputs_mask_keeps_intermediates_on_device(gpu, oracle):
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 20)
+    _, nodes = _layer(ga, oracle)
+    want = _sequential(ga, nodes)
+    for _, _, d in nodes:
+        ga.setTensorBytes(d, np.zeros(4 * d.ne[1], np.uint8))
+    outs = [d.name in ("o", "d") for _, _, d in nodes]
+    g = G.ResidentGraph(ga, nodes, outputs=outs)
+    g.compute()
+    for (_, _, d), w, o in zip(nodes, want, outs):
+        got = bytes(ga.tensorBytes(d))
+        assert got == (w if o else bytes(len(w))), d.name
+    assert g.transferBytes(False) == 4 * 256 * 2
+
+
+def test_f32_chain_and_war_hazard(gpu):
+    """An F32 x F32 node whose A is an earlier node's dst, and a node that overwrites the
+    bytes an earlier node reads (it must run after the read)."""
+    import ggml_hip as G
+    rng = np.random.default_rng(1)
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 16)
+    a0 = ga.allocateTensor(G.GGMLType.F32, [32, 16])
+    b0 = ga.allocateTensor(G.GGMLType.F32, [8, 32])
+    d0 = ga.allocateTensor(G.GGMLType.F32, [8, 16])       # = A of node 1 viewed as [K=8, M=16]
+    b1 = ga.allocateTensor(G.GGMLType.F32, [3, 8])
+    d1 = ga.allocateTensor(G.GGMLType.F32, [3, 16])
+    a2 = ga.allocateTensor(G.GGMLType.F32, [8, 4])
+    b2 = ga.allocateTensor(G.GGMLType.F32, [3, 8])
+    for t in (a0, b0, b1, a2, b2):
+        ga.setTensorBytes(t, rng.standard_normal(t.ne[0] * t.ne[1]).astype(np.float32))
+    a1 = G.GGMLTensor(G.GGMLType.F32, [8, 16], bufferId=d0.bufferId, dataOffset=d0.dataOffset)
+    # node 2 writes into b1's bytes after node 1 read them (WAR): [N=3, M=4] = 48 B of b1's 96
+    d2 = G.GGMLTensor(G.GGMLType.F32, [3, 4], bufferId=b1.bufferId, dataOffset=b1.dataOffset)
+    nodes = [(a0, b0, d0), (a1, b1, d1), (a2, b2, d2)]
+    snap = ga.buffers[0].copy()
+    want = _sequential(ga, nodes)
+    ga.buffers[0][:] = snap
+    g = G.ResidentGraph(ga, nodes)
+    assert g.numLevels == 3  # node 2 overwrites the b1 bytes node 1 reads: after node 1
+    g.compute()
+    assert [bytes(ga.tensorBytes(d)) for _, _, d in nodes] == want
+
+
+def test_strided_dst_gap_bytes_survive(gpu, oracle):
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 16)
+    M, K, N = 40, 128, 2
+    a = ga.allocateTensor(G.GGMLType.Q4_0, [K, M])
+    ga.setTensorBytes(a, oracle.quantize(2, random_weights(M * K, 5)))
+    b = ga.allocateTensor(G.GGMLType.F32, [N, K])
+    ga.setTensorBytes(b, random_acts(N * K, 6))
+    raw = ga.allocateTensor(G.GGMLType.F32, [N + 3, M])  # rows padded by 3 floats of sentinel
+    ga.setTensorBytes(raw, np.full((N + 3) * M, 7.25, np.float32))
+    d = G.GGMLTensor(G.GGMLType.F32, [N, M], nb=[4, 4 * (N + 3), 4 * (N + 3) * M, 4 * (N + 3) * M],
+                     bufferId=raw.bufferId, dataOffset=raw.dataOffset)
+    g = G.ResidentGraph(ga, [(a, b, d)])
+    g.compute()
+    out = np.frombuffer(bytes(ga.tensorBytes(raw)), np.float32).reshape(M, N + 3)
+    assert np.all(out[:, N:] == 7.25)
+    got = out[:, :N].copy()
+    ga.setTensorBytes(raw, np.full((N + 3) * M, 7.25, np.float32))
+    G.computeMatMul(ga, ga.context, a, b, d)
+    ref = np.frombuffer(bytes(ga.tensorBytes(raw)), np.float32).reshape(M, N + 3)[:, :N]
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_backend_graph_compute_host_uses_resident_graph(gpu, oracle):
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 20)
+    _, nodes = _layer(ga, oracle)
+    want = _sequential(ga, nodes)
+    dsts = []
+    for a, b, d in nodes:
+        d.op, d.src = G.GGMLOp.MUL_MAT, [a, b]
+        ga.setTensorBytes(d, np.zeros(4 * d.ne[1], np.uint8))
+        dsts.append(d)
+    be = G.GGMLHipBackend(ga)
+    assert be.graphCompute(G.GGMLCGraph(dsts, ga)) == G.GGMLStatus.SUCCESS
+    assert [bytes(ga.tensorBytes(d)) for d in dsts] == want
