@@ -442,6 +442,63 @@ int launch_gemm_qt(const GemmArgs &g, const XSplitArgs &xa, bool lds_ok, hipStre
   return launch_gemm_t<QT, 2, 2, 2, 2>(g, xa, st);
 }
 
+// Skinny split-K GEMM (gemm_skinny_kernel): 2 <= N <= 32, whole blocks, weight rows and slice
+// pieces 16-byte aligned (buffer offset % 16 == 0, row bytes % 16 == 0: every Llama shape).
+bool skinny_eligible(const lk_tensor *a, const Checked &c) {
+  static const bool off = getenv("LK_NO_SKINNY") != nullptr;  // tuning / A-B only
+  if (off || c.N > 32) return false;
+  const uint64_t bb = a->type == LK_TYPE_Q4_0 ? 18 : a->type == LK_TYPE_Q4_1 ? 20 : 34;
+  const uint64_t rb = (uint64_t)(c.K / 32) * bb;
+  const uintptr_t base = (uintptr_t)a->data + a->data_offset;
+  return base % 16 == 0 && rb % 16 == 0 && rb * 16 < (1ull << 31);
+}
+
+template <int QT, int NT>
+int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
+  using SG = SkinnyGeom<QT, NT>;
+  GemmScratch &S = gemm_scratch();
+  const int nblk = g.K / 32;
+  const int slices = (nblk + SG::SB - 1) / SG::SB;
+  const int ntile = (g.M + 15) / 16;
+  // one workgroup per CU (LDS): about cu_count() workgroups in all
+  int ranges = std::max(1, std::min(ntile, (cu_count() + slices - 1) / slices));
+  g.tiles_per_range = (ntile + ranges - 1) / ranges;
+  ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
+  g.slices = slices;
+  if (slices > 1) {
+    const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
+    if (rc) return rc;
+    g.partial = (float *)S.partial;
+  }
+  g.tasks = ranges * slices;
+  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  hipLaunchKernelGGL((gemm_skinny_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
+  if (slices > 1) {
+    const int64_t threads = (int64_t)g.M * (16 * NT / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
+                       slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  SkinnyArgs g{};
+  g.a = (const uint8_t *)a->data + a->data_offset;
+  g.b = (const uint8_t *)b->data + b->data_offset;
+  g.b_nb0 = b->nb[0]; g.b_nb1 = b->nb[1];
+  g.dst = (uint8_t *)dst->data + dst->data_offset;
+  g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
+  g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
+  const bool one = c.N <= 16;
+  switch (a->type) {
+    case LK_TYPE_Q4_0: return one ? launch_skinny_t<LK_TYPE_Q4_0, 1>(g, st) : launch_skinny_t<LK_TYPE_Q4_0, 2>(g, st);
+    case LK_TYPE_Q4_1: return one ? launch_skinny_t<LK_TYPE_Q4_1, 1>(g, st) : launch_skinny_t<LK_TYPE_Q4_1, 2>(g, st);
+    case LK_TYPE_Q8_0: return one ? launch_skinny_t<LK_TYPE_Q8_0, 1>(g, st) : launch_skinny_t<LK_TYPE_Q8_0, 2>(g, st);
+    default: return fail(LK_ERR_NOT_IMPLEMENTED, "skinny gemm: type %d", a->type);
+  }
+}
+
 int launch_gemm(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   GemmScratch &S = gemm_scratch();
   const int64_t nblk = c.K / 32, ntx = (c.N + 15) / 16;
@@ -522,7 +579,7 @@ int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *ds
     return launch_generic(a, b, dst, c, st);
   }
   if (gemv_eligible(a, b, dst, c)) return run_single_gemv(a, b, dst, c, st);
-  if (gemm_eligible(c)) return launch_gemm(a, b, dst, c, st);
+  if (gemm_eligible(c)) return skinny_eligible(a, c) ? launch_skinny(a, b, dst, c, st) : launch_gemm(a, b, dst, c, st);
   return launch_generic(a, b, dst, c, st);
 }
 

@@ -882,6 +882,11 @@ __global__ __launch_bounds__(256) void gemm_q_mfma_kernel(GemmArgs g) {
 template <bool NT>
 __device__ __forceinline__ void dma16(const void *sbase, uint32_t vofs, const void *lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LK_LDS const void *)lds_dst);
+  // the base must live in SGPRs; say so even where uniformity analysis cannot prove it
+  const uint64_t sb = (uint64_t)(uintptr_t)sbase;
+  const uint32_t sb_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);  // (readfirstlane returns int:
+  const uint32_t sb_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));  //  no sign extension)
+  sbase = (const void *)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo);
   if constexpr (NT) asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
   else asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
 }
@@ -1033,6 +1038,388 @@ __global__ __launch_bounds__(NW * 64) void gemm_q_lds_kernel(GemmArgs g) {
     wait_vmcnt<0>();  // drain the padding stages before the workgroup's LDS is released
   }
   gemm_finish<MT, NT, BM, BN>(g, acc, tile, tiles, slice, tm, tn, wave, 0, wave, lane);
+}
+
+// ---- skinny batched GEMM (2 <= N <= 32): split-K, activations held in VGPRs ---------------
+//
+// C3's shape (M 11,008, K 4,096, N 32) is still bound by HBM (114 flop per weight byte). Its
+// weight stream only runs near HBM speed when each row's DMA piece is long — pieces that
+// straddle 128-B lines are fetched twice under `nt` (16 rows x 144 B stream at 3.8 TB/s,
+// 8 x 288 B at 5.6, 1 x 2,304 B at 6.3: tools/lab/pieces.hip) — and re-reading the
+// activations per 16-row tile from LDS left every block waiting on an LDS round trip. So:
+//
+//   workgroup (range r, slice s): rows of range r x blocks [s·SB, s·SB + SB) of K, one wave
+//     per SIMD (4 waves, up to 512 VGPRs each).
+//   prologue: each wave starts its weight stream (LDS-DMA), the workgroup converts the slice's
+//     activations x(n, k) once into bf16 hi/lo MFMA fragments (x = hi + lo, |x - hi - lo| <=
+//     2^-17|x|) staged in LDS, and every wave then holds ALL of them in VGPRs (SB·NT·2·4 =
+//     256 VGPRs at N 32): in the main loop only the weight codes come from LDS.
+//   main loop: a wave takes one 16-row tile at a time; its unit (16 rows x SB·BB bytes: 288 B
+//     per row for Q4_0) lands in the wave's ring of D slots; per block and 16-column x-tile,
+//     two v_mfma_f32_16x16x32_bf16 (lo, hi) on exact weight codes, then acc += scale·p:
+//       Q4_0: codes (n - 8)·2^-9 (fp8 conversion of the nibble, minus 2^-6), scale 512·d;
+//       Q4_1: codes n·2^-9, scale 512·d, plus m·Σx (Σx per block and column, from LDS);
+//       Q8_0: codes q, scale d.
+//   output: one slice -> dst directly; otherwise an f32 partial slab P[s][m][n] per slice and
+//     splitk_reduce_kernel sums the slabs in slice order (deterministic).
+//
+// A slot holds the unit row-major at a pitch of one extra 16-B cell per row (lanes of one DMA
+// instruction read consecutive 16-B pieces of a row; the pad cell keeps the 16 rows' dwords at
+// one block offset 2-way bank-conflicted at worst). At the start of a unit a wave reads every
+// dword its blocks need (WPB per block) with one burst of LDS reads and one wait.
+
+// Weight DMA policy of the skinny GEMM: default (0) keeps lines in L2, where the neighbouring
+// slice's workgroup (same XCD) reads the 128-B line its piece shares with this one.
+#ifndef LK_SKINNY_NT
+#define LK_SKINNY_NT 0
+#endif
+
+template <int QT, int NT> struct SkinnyGeom {
+  static constexpr int NW = 4;                         // waves per workgroup: one per SIMD
+  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr int SB = 16;                        // blocks per K slice
+  static constexpr int RP = SB * BB;                   // row bytes of one unit (a multiple of 16)
+  static constexpr int PPR = RP / 16;                  // 16-B pieces per row
+  static constexpr int PITCH = RP + 16;                // LDS row pitch: one pad cell per row (banks)
+  static constexpr int L = (16 * (PPR + 1) + 63) / 64; // DMA instructions per unit
+  static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;  // code/scale dwords per block
+  static constexpr int SLOT = L * 1024;
+  static constexpr int XB = SB * NT * kXSplits * 1024; // activation fragments (staging)
+  static constexpr int TB = SB * NT * 16 * 4;          // Σx per (block, column) (Q4_1)
+  static constexpr int DFIT = (kLdsBytes - XB - TB) / (NW * SLOT);
+  static constexpr int D = DFIT > 4 ? 4 : DFIT;         // ring depth (units per wave)
+  static constexpr int LDS = XB + TB + NW * D * SLOT;
+  static constexpr int FPW = SB * NT / NW;             // fragments each wave converts
+  static_assert(RP % 16 == 0, "row pieces");
+  static_assert(D >= 2, "ring must double-buffer");
+  static_assert((SB * NT) % NW == 0, "fragments per wave");
+  static_assert((D - 1) * L + D * NT < 64, "vmcnt");
+};
+
+struct SkinnyArgs {
+  const uint8_t *a;        // weights (buffer base + dataOffset), rows RB bytes apart
+  const uint8_t *b;        // B(n, k) at n·b_nb0 + k·b_nb1
+  int64_t b_nb0, b_nb1;
+  uint8_t *dst;            // dst(n, m) at n·d_nb0 + m·d_nb1
+  int64_t d_nb0, d_nb1;
+  float *partial;          // [slices][M][16·NT] when slices > 1
+  int32_t M, N, K;
+  int32_t slices, tiles_per_range, tasks;  // tasks = ranges·slices (the grid is padded to 8)
+};
+
+// s_waitcnt vmcnt(BASE + j·STEP) for a run-time j in [0, J].
+template <int BASE, int STEP, int J> __device__ __forceinline__ void wait_vmcnt_prog(int j) {
+  if (j >= J) wait_vmcnt<BASE + J * STEP>();
+  else if constexpr (J > 0) wait_vmcnt_prog<BASE, STEP, J - 1>(j);
+}
+
+// Q4_0 weight fragment with the offset folded in: (n - 8)·2^-9, exact in bf16, k order
+// (0,2,4,6,1,3,5,7) as Q4Frag.
+__device__ __forceinline__ bf16x8 q4_0_frag_biased(uint32_t u) {
+  const uint32_t lo = u & 0x0F0F0F0Fu, hi = (u >> 4) & 0x0F0F0F0Fu;
+  const f2v bias = {-0.015625f, -0.015625f};
+  const f2v e0 = fp8x2<false>(lo) + bias, e1 = fp8x2<true>(lo) + bias, o0 = fp8x2<false>(hi) + bias,
+            o1 = fp8x2<true>(hi) + bias;
+  uint32_t w[4] = {pack_bf16_exact(e0.x, e0.y), pack_bf16_exact(e1.x, e1.y), pack_bf16_exact(o0.x, o0.y),
+                   pack_bf16_exact(o1.x, o1.y)};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+// The WPB dwords of block B for lane (row m = lane & 15, group g = lane >> 4): bm = slot + m·PITCH,
+// bg = bm + (4 or 8)·g. The caller issues every block's reads, then a compiler barrier, so they
+// go out as one burst (the compiler would otherwise sink each next to its use).
+template <int QT, int B, int WPB>
+__device__ __forceinline__ void skinny_read(const uint8_t *bm, const uint8_t *bg, uint32_t (&w)[WPB]) {
+  constexpr int OB = B * QTraits<QT>::BB;  // block offset within the row piece
+#define LK_DSR(i, base, off) w[i] = *(const uint32_t *)((base) + (off))
+  if constexpr (QT == LK_TYPE_Q4_1) {        // (d, m) dword; codes at +4 + 4g
+    LK_DSR(0, bm, OB);
+    LK_DSR(1, bg, OB + 4);
+  } else if constexpr (QT == LK_TYPE_Q4_0) {
+    if constexpr ((OB & 3) == 0) {           // d lo; codes at +2 + 4g: two dwords, realigned by 2
+      LK_DSR(0, bm, OB);
+      LK_DSR(1, bg, OB);
+      LK_DSR(2, bg, OB + 4);
+    } else {                                 // d in the high half of the dword before; codes aligned
+      LK_DSR(0, bm, OB - 2);
+      LK_DSR(1, bg, OB + 2);
+      w[2] = 0;
+    }
+  } else {                                   // Q8_0: codes bytes [2 + 8g, 10 + 8g)
+    if constexpr ((OB & 3) == 0) {
+      LK_DSR(0, bm, OB);
+      LK_DSR(1, bg, OB);
+      LK_DSR(2, bg, OB + 4);
+      LK_DSR(3, bg, OB + 8);
+    } else {
+      LK_DSR(0, bm, OB - 2);
+      LK_DSR(1, bg, OB + 2);
+      LK_DSR(2, bg, OB + 6);
+      w[3] = 0;
+    }
+  }
+#undef LK_DSR
+}
+
+template <int QT, int SB, int WPB, int B>
+__device__ __forceinline__ void skinny_read_all(const uint8_t *bm, const uint8_t *bg, uint32_t (&w)[SB][WPB]) {
+  if constexpr (B < SB) {
+    skinny_read<QT, B, WPB>(bm, bg, w[B]);
+    skinny_read_all<QT, SB, WPB, B + 1>(bm, bg, w);
+  }
+}
+
+// Block B: weight fragment from its dwords, MFMAs against the held activation fragments, scaled
+// accumulation.
+template <int QT, int NT, int B, int WPB>
+__device__ __forceinline__ void skinny_block(const uint32_t (&w)[WPB], const float *tlds, int lane, const u32x4 (&xh)[16][NT],
+                                             const u32x4 (&xl)[16][NT], f32x4 (&acc)[NT]) {
+  constexpr int OB = B * QTraits<QT>::BB;
+  bf16x8 wf;
+  float s1, s2 = 0.f;
+  if constexpr (QT == LK_TYPE_Q4_1) {
+    wf = Q4Frag<0>::make(w[1]);
+    s1 = 512.f * h2f(w[0]);
+    s2 = h2f(w[0] >> 16);
+  } else if constexpr (QT == LK_TYPE_Q4_0) {
+    if constexpr ((OB & 3) == 0) {
+      wf = q4_0_frag_biased(align2(w[2], w[1]));
+      s1 = 512.f * h2f(w[0]);
+    } else {
+      wf = q4_0_frag_biased(w[1]);
+      s1 = 512.f * h2f(w[0] >> 16);
+    }
+  } else {
+    if constexpr ((OB & 3) == 0) {
+      wf = w_frag<LK_TYPE_Q8_0>(align2(w[2], w[1]), align2(w[3], w[2]));
+      s1 = h2f(w[0]);
+    } else {
+      wf = w_frag<LK_TYPE_Q8_0>(w[1], w[2]);
+      s1 = h2f(w[0] >> 16);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf, f32x4{0.f, 0.f, 0.f, 0.f},
+                                                      0, 0, 0);
+    p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (QT == LK_TYPE_Q4_1) t = *(const f32x4 *)(tlds + (B * NT + j) * 16 + (lane >> 4) * 4);
+    accumulate<QT == LK_TYPE_Q4_1>(acc[j], s1, s2, p, t);
+  }
+}
+
+// Blocks B..nb-1 of a unit, unrolled at compile time. FULL: nb == SB (no guards).
+template <int QT, int NT, int SB, int WPB, bool FULL, int B>
+__device__ __forceinline__ void skinny_blocks(const uint32_t (&w)[SB][WPB], const float *tlds, int nb, int lane,
+                                              const u32x4 (&xh)[16][NT], const u32x4 (&xl)[16][NT], f32x4 (&acc)[NT]) {
+  if constexpr (B < SB) {
+    if (!FULL && B >= nb) return;
+    skinny_block<QT, NT, B, WPB>(w[B], tlds, lane, xh, xl, acc);
+    skinny_blocks<QT, NT, SB, WPB, FULL, B + 1>(w, tlds, nb, lane, xh, xl, acc);
+  }
+}
+
+#ifdef LK_SKINNY_TRACE
+__device__ uint64_t *lk_strace_buf;
+#endif
+
+template <int QT, int NT>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
+  using G = SkinnyGeom<QT, NT>;
+  constexpr int BB = G::BB, SB = G::SB, D = G::D, L = G::L, NW = G::NW;
+  static_assert(SB == 16, "held activation arrays are [16][NT]");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t *xlds = smem;
+  float *tlds = (float *)(smem + G::XB);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t *ring = smem + G::XB + G::TB + wave * D * G::SLOT;
+#ifdef LK_SKINNY_TRACE
+  // the buffer pointer is read once, by a scalar load (a vector load would wait behind the DMA)
+  uint64_t *const strace = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_strace_buf)[0];
+#define LK_STRACE(slot_)                                                                                     \
+  do {                                                                                                      \
+    if (lane == 0 && strace)                                                                                \
+      strace[((size_t)blockIdx.x * NW + wave) * 8 + (slot_)] = __builtin_amdgcn_s_memrealtime();             \
+  } while (0)
+#else
+#define LK_STRACE(slot_) do {} while (0)
+#endif
+  LK_STRACE(0);
+  // XCD-aware task order (speed only: dispatch is observed round-robin over the 8 XCDs):
+  // workgroup b runs task (b % 8)·(grid / 8) + b / 8, so the slices of one row range — which
+  // share the 128-B lines at their boundaries — and a range's neighbours land on one L2.
+  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+  if (task >= g.tasks) return;  // grid padding (before any barrier: the whole workgroup leaves)
+  const int slice = task % g.slices, range = task / g.slices;
+  const int nblk = g.K / 32;
+  const int kb0 = slice * SB, nb = min(SB, nblk - kb0);
+  const int64_t RB = (int64_t)nblk * BB;
+  const int ntile = (g.M + 15) / 16;
+  const int t0 = range * g.tiles_per_range, t1 = min(t0 + g.tiles_per_range, ntile);
+  // this wave's tiles: t0 + wave + i·NW
+  const int nunits = t1 - t0 - wave > 0 ? (t1 - t0 - wave + NW - 1) / NW : 0;
+  const int ppr = nb * BB / 16;  // 16-B pieces per row in this slice (the last slice may be short)
+
+  // unit u = the wave's u-th tile's slice: lane q of the unit's DMA lands at cell q = r·(PPR+1) + c
+  // (row r, piece c); pad cells and pieces past a short slice re-read the row's first piece
+  const uint8_t *abase = g.a + (int64_t)kb0 * BB;
+  uint32_t rofs[L];  // per-lane byte offset of its piece from the tile's first row (the tile's
+  int rrow[L];       // rows past M read row M-1 instead)
+#pragma unroll
+  for (int j = 0; j < L; j++) {
+    const int q = j * 64 + lane, r = q / (G::PPR + 1), c = q % (G::PPR + 1);
+    rrow[j] = min(r, 15);
+    rofs[j] = (uint32_t)((c < ppr && r < 16) ? c * 16 : 0);
+  }
+  auto issue = [&](int u, int sl) __attribute__((always_inline)) {
+    const int t = t0 + wave + u * NW;
+    const uint8_t *tb = abase + (int64_t)t * 16 * RB;
+    const int rmax = g.M - 1 - t * 16;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
+      dma16<LK_SKINNY_NT>(tb, vofs, ring + sl * G::SLOT + j * 1024);
+    }
+  };
+  // 1. the HBM stream starts with one unit per wave
+  if (nunits > 0) issue(0, 0);
+
+  // 2. activations of the slice -> LDS fragments (x-tile j, block b, split s): lane l holds
+  // x(n = 16j + (l & 15), k = 32(kb0 + b) + 8(l >> 4) + order[0..7]) as bf16 hi / lo. Fragment
+  // f = b·NT + j is converted by wave f % NW; all its loads are issued before any is used.
+  float v[G::FPW][8];
+#pragma unroll
+  for (int i = 0; i < G::FPW; i++) {
+    const int f = wave + i * NW, b = f / NT, j = f % NT;
+    const int n = 16 * j + (lane & 15);
+    const int64_t k0 = 32 * (int64_t)(kb0 + b) + 8 * (lane >> 4);
+    const bool ok = b < nb && n < g.N;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int kk = (QT != LK_TYPE_Q8_0) ? ((e & 3) * 2 + (e >> 2)) : e;
+      v[i][e] = ok ? *(const float *)(g.b + n * g.b_nb0 + (k0 + kk) * g.b_nb1) : 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < G::FPW; i++) {
+    const int f = wave + i * NW;
+    float part = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; e++) part += v[i][e];
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      uint32_t h[2], l[2];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t bx = __builtin_bit_cast(uint32_t, v[i][e + q]);
+        const float r = v[i][e + q] - __builtin_bit_cast(float, bx & 0xFFFF0000u);  // exact
+        uint32_t br = __builtin_bit_cast(uint32_t, r);
+        br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even
+        h[q] = bx;
+        l[q] = br;
+      }
+      hi[e / 2] = __builtin_amdgcn_perm(h[1], h[0], 0x07060302u);
+      lo[e / 2] = __builtin_amdgcn_perm(l[1], l[0], 0x07060302u);
+    }
+    u32x4 *xf = (u32x4 *)(xlds + (f * kXSplits) * 1024) + lane;
+    xf[0] = u32x4{hi[0], hi[1], hi[2], hi[3]};
+    xf[64] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+    if constexpr (QT == LK_TYPE_Q4_1) {
+      part += __shfl_xor(part, 16, kWave);
+      part += __shfl_xor(part, 32, kWave);
+      if (lane < 16) tlds[f * 16 + lane] = part;
+    }
+  }
+  LK_STRACE(1);
+  // 3. the rest of the ring
+  for (int u = 1; u < min(D, nunits); u++) issue(u, u);
+  wait_lgkmcnt0();
+  __builtin_amdgcn_s_barrier();
+  LK_STRACE(2);
+  // 4. every wave holds all of the slice's activation fragments
+  u32x4 xh[16][NT], xl[16][NT];
+#pragma unroll
+  for (int b = 0; b < SB; b++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const u32x4 *xf = (const u32x4 *)(xlds + ((b * NT + j) * kXSplits) * 1024) + lane;
+      xh[b][j] = xf[0];
+      xl[b][j] = xf[64];
+    }
+
+  const int N16 = 16 * NT;
+  int slot = 0;
+  for (int u = 0; u < nunits; u++) {
+    // ops younger than unit u's DMA (issue order: units 0..D-1 in the prologue, then per tile
+    // i: unit i+D, the stores of tile i): units u+1..u+D-1 (L each) and the stores of the
+    // min(u, D) previous tiles (>= NT each); short of that steady state (the last units) drain
+    if (u + D - 1 < nunits) wait_vmcnt_prog<(D - 1) * L, NT, D>(u);
+    else wait_vmcnt<0>();
+    asm volatile("" ::: "memory");  // the slot's LDS reads stay behind the wait
+    if (u == 0) LK_STRACE(3);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint32_t wd[SB][G::WPB];
+    {
+      const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::PITCH;
+      const uint8_t *bg = bm + (QT == LK_TYPE_Q8_0 ? 8 : 4) * (lane >> 4);
+      skinny_read_all<QT, SB, G::WPB, 0>(bm, bg, wd);
+      asm volatile("" ::: "memory");  // keep the burst together: no read sinks below this line
+    }
+    if (nb == SB) skinny_blocks<QT, NT, SB, G::WPB, true, 0>(wd, tlds, nb, lane, xh, xl, acc);
+    else skinny_blocks<QT, NT, SB, G::WPB, false, 0>(wd, tlds, nb, lane, xh, xl, acc);
+    if (u == 0) LK_STRACE(7);
+    wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
+    if (u + D < nunits) issue(u + D, slot);
+    slot = (slot + 1 == D) ? 0 : slot + 1;
+    // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
+    const int t = t0 + wave + u * NW;
+    const int64_t m = (int64_t)t * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int n0 = 16 * j + 4 * (lane >> 4);
+      if (g.slices > 1) {
+        if (m < g.M) *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = acc[j];
+      } else if (m < g.M) {
+        const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+      }
+    }
+    if (u == 0) LK_STRACE(4);
+  }
+  LK_STRACE(5);
+  wait_vmcnt<0>();
+  LK_STRACE(6);
+#undef LK_STRACE
+}
+
+// dst(n, m) = Σ_s P[s][m][n], slices in order (deterministic); one thread per 4 columns.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restrict__ P, int slices, int M, int N, int N16,
+                                                            uint8_t *__restrict__ dst, int64_t d_nb0, int64_t d_nb1) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c4 = N16 / 4;
+  if (idx >= (int64_t)M * c4) return;
+  const int64_t m = idx / c4;
+  const int n0 = (int)(idx % c4) * 4;
+  f32x4 s = *(const f32x4 *)(P + m * N16 + n0);
+  for (int sl = 1; sl < slices; sl++) {
+    const f32x4 v = *(const f32x4 *)(P + ((int64_t)sl * M + m) * N16 + n0);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const float e4[4] = {s.x, s.y, s.z, s.w};
+  if (d_nb0 == 4 && n0 + 4 <= N && (((uintptr_t)(dst + m * d_nb1 + n0 * 4)) & 15) == 0) {
+    *(f32x4 *)(dst + m * d_nb1 + n0 * 4) = s;
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    if (n0 + q < N) *(float *)(dst + m * d_nb1 + (n0 + q) * d_nb0) = e4[q];
 }
 
 // ---- generic path (any K, any byte strides, ragged blocks) ----------------------

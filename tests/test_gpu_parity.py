@@ -323,3 +323,41 @@ def test_full_size_linearity(gpu, oracle):
     y12 = gpu_matmul(qt, q, M, K, 1, (x1 + x2).astype(np.float32))
     ok, msg = parity_ok(y12, (y1.astype(np.float64) + y2))
     assert ok, msg
+
+
+# Skinny split-K GEMM (2 <= N <= 32, 16-byte-aligned rows): ragged K slices, ragged tiles,
+# one-slice direct stores, strided operands; misaligned weights fall back to the LDS GEMM.
+SKINNY = [
+    (1000, 11008, 2),   # 344 blocks: 21 full K slices and a half one
+    (4096, 4096, 16),   # exactly one 16-column x-tile
+    (257, 4096, 31),    # ragged rows (a 1-row tile) and columns (two x-tiles)
+    (40, 512, 5),       # one K slice: outputs stored without the reduce kernel
+    (3000, 2048, 32),
+]
+
+
+@pytest.mark.parametrize("qt", Q_TYPES, ids=lambda t: QNAME[t])
+@pytest.mark.parametrize("shape", SKINNY, ids=lambda s: "x".join(map(str, s)))
+def test_skinny_gemm_vs_oracle(gpu, oracle, qt, shape):
+    M, K, N = shape
+    q, x = make_inputs(oracle, qt, M, K, N, seed=M + N)
+    ref = oracle.mat_mul_q(qt, q, M, K, x, tight=True)
+    noise = noise_for(oracle, qt, q, M, K, x)
+    got = gpu_matmul(qt, q, M, K, N, x)
+    ok, msg = parity_ok(got, ref, noise=noise)
+    assert ok, msg
+    again = gpu_matmul(qt, q, M, K, N, x)
+    assert np.array_equal(got.view(np.uint32), again.view(np.uint32)), "split-K reduction is not deterministic"
+
+
+@pytest.mark.parametrize("qt", Q_TYPES, ids=lambda t: QNAME[t])
+def test_skinny_gemm_offsets_strides(gpu, oracle, qt):
+    M, K, N = 100, 1024, 9
+    q, x = make_inputs(oracle, qt, M, K, N, seed=11)
+    ref = oracle.mat_mul_q(qt, q, M, K, x)
+    noise = noise_for(oracle, qt, q, M, K, x)
+    for kw in [dict(a_off=16, b_off=32, d_off=48), dict(a_off=2), dict(b_off=4), dict(dst_row_pad=3),
+               dict(b_stride=11), dict(host=True, a_off=32, dst_row_pad=1)]:
+        got = gpu_matmul(qt, q, M, K, N, x, **kw)
+        ok, msg = parity_ok(got, ref, noise=noise)
+        assert ok, (kw, msg)

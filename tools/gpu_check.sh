@@ -13,7 +13,7 @@ step() {  # step <name> <seconds> <cmd...>
   if [ $rc -ne 0 ]; then echo "stopping after rc=$rc"; exit $rc; fi
   return 0
 }
-[ -z "$NO_TESTS" ] && step pytest_gpu 900 python -m pytest tests -q -m gpu -x
+[ -z "$NO_TESTS" ] && step pytest_gpu 900 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread
 [ -n "$SMOKE" ] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 5
 [ -n "$PROF" ] && step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 20 --warmup 5 --no-headline --no-chain --no-batched --no-cpu-baseline
