@@ -499,6 +499,65 @@ int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   }
 }
 
+// Wide GEMM (gemm_wide_kernel): N > 32, K % 128 == 0, weight rows 8-byte aligned, and the
+// last row's 80-byte window may read OVERREAD bytes past the matrix: they must be in the buffer.
+bool wide_eligible(const lk_tensor *a, const Checked &c) {
+  static const bool off = getenv("LK_NO_WIDE") != nullptr;  // tuning / A-B only
+  if (off || c.N <= 32 || (c.K / 32) % 4) return false;
+  const uint64_t bb = block_bytes(a->type);
+  const uintptr_t base = (uintptr_t)a->data + a->data_offset;
+  const uint64_t over = a->type == LK_TYPE_Q4_0 ? WideGeom<LK_TYPE_Q4_0>::OVERREAD
+                       : a->type == LK_TYPE_Q4_1 ? WideGeom<LK_TYPE_Q4_1>::OVERREAD
+                                                 : WideGeom<LK_TYPE_Q8_0>::OVERREAD;
+  const uint64_t rb = (uint64_t)(c.K / 32) * bb;
+  return base % 8 == 0 && rb % 8 == 0 && (uint64_t)c.M * rb < (1ull << 31) && c.a_hi + over <= a->buf_bytes;
+}
+
+template <int QT>
+int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
+  using WG = WideGeom<QT>;
+  GemmScratch &S = gemm_scratch();
+  g.tiles_m = (g.M + WG::BM - 1) / WG::BM;
+  g.tiles_n = (g.N + WG::BN - 1) / WG::BN;
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int nst = g.K / 32 / WG::SB;  // stages over the whole K
+  int slices = std::max(1, std::min({(cu_count() + tiles - 1) / tiles, 16, nst}));
+  g.kslice = ((nst + slices - 1) / slices) * WG::SB;
+  slices = (g.K / 32 + g.kslice - 1) / g.kslice;
+  g.slices = slices;
+  const int npad = g.tiles_n * WG::BN;
+  if (slices > 1) {
+    const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * npad * sizeof(float));
+    if (rc) return rc;
+    g.partial = (float *)S.partial;
+  }
+  // super-tile per XCD: sm x sn tiles (all slices), minimising the XCD's L2 footprint per k:
+  // sn·BN·4 B of activation fragments + sm·BM·BB/32 B of weights
+  const int per_xcd = (tiles + 7) / 8;
+  int best = 1;
+  double cost = 1e30;
+  for (int sn = 1; sn <= g.tiles_n; sn++) {
+    const int sm = std::min(g.tiles_m, (per_xcd + sn - 1) / sn);
+    const double c = sn * WG::BN * 4.0 + sm * WG::BM * (WG::BB / 32.0);
+    if (sm * sn >= per_xcd && c < cost) { cost = c; best = sn; }
+  }
+  g.sn = best;
+  g.sm = std::min(g.tiles_m, (per_xcd + best - 1) / best);
+  const int nsuper = ((g.tiles_m + g.sm - 1) / g.sm) * ((g.tiles_n + g.sn - 1) / g.sn);
+  g.tasks = nsuper * g.sm * g.sn * slices;
+  const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
+  if (slices > 1) {
+    const int64_t threads = (int64_t)g.M * (npad / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
+                       slices, g.M, g.N, npad, g.dst, g.d_nb0, g.d_nb1);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
 int launch_gemm(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   GemmScratch &S = gemm_scratch();
   const int64_t nblk = c.K / 32, ntx = (c.N + 15) / 16;
@@ -513,6 +572,21 @@ int launch_gemm(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   xa.xsum = (float *)((uint8_t *)S.frag + fb);
   xa.mult = a->type == LK_TYPE_Q4_0 ? GemmQ<LK_TYPE_Q4_0>::MULT : 1.f;
   xa.q4_order = a->type != LK_TYPE_Q8_0;
+  if (wide_eligible(a, c)) {
+    WideArgs w{};
+    w.a = (const uint8_t *)a->data + a->data_offset;
+    w.frag = xa.frag;
+    w.xsum = xa.xsum;
+    w.dst = (uint8_t *)dst->data + dst->data_offset;
+    w.d_nb0 = dst->nb[0]; w.d_nb1 = dst->nb[1];
+    w.M = (int32_t)c.M; w.N = (int32_t)c.N; w.K = (int32_t)c.K;
+    switch (a->type) {
+      case LK_TYPE_Q4_0: return launch_wide_t<LK_TYPE_Q4_0>(w, xa, st);
+      case LK_TYPE_Q4_1: return launch_wide_t<LK_TYPE_Q4_1>(w, xa, st);
+      case LK_TYPE_Q8_0: return launch_wide_t<LK_TYPE_Q8_0>(w, xa, st);
+      default: break;
+    }
+  }
   const bool lds_ok = gemm_lds_eligible(a->type, a, c);
   GemmArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;

@@ -742,6 +742,19 @@ __device__ __forceinline__ void accumulate(f32x4 &acc, float s1, float s2, f32x4
   acc = f32x4{a0.x, a0.y, a1.x, a1.y};
 }
 
+// acc += s1·p (+ s2·T for Q4_1) as four scalar FMAs: v_pk_fma_f32 beside MFMAs costs more
+// issue time than two v_fma_f32 (MI355X_MICROARCH.md, cycle constants), and the library is
+// built with -fno-slp-vectorize so the compiler does not pack these back.
+template <bool HAS_MIN>
+__device__ __forceinline__ void accumulate_s(f32x4 &acc, float s1, float s2, f32x4 p, f32x4 t) {
+  if constexpr (HAS_MIN) {
+    acc.x = fmaf(s2, t.x, acc.x); acc.y = fmaf(s2, t.y, acc.y);
+    acc.z = fmaf(s2, t.z, acc.z); acc.w = fmaf(s2, t.w, acc.w);
+  }
+  acc.x = fmaf(s1, p.x, acc.x); acc.y = fmaf(s1, p.y, acc.y);
+  acc.z = fmaf(s1, p.z, acc.z); acc.w = fmaf(s1, p.w, acc.w);
+}
+
 // Epilogue shared by the GEMM kernels: lane holds C'(n = 16·xtile + 4(lane>>4) + e, m = row),
 // e = 0..3. slices == 1: store. Split-K: publish this slice's tile; the last slice to arrive sums
 // all slices in slice order (deterministic) and stores, then re-arms the tile counter.
@@ -1397,6 +1410,297 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
   wait_vmcnt<0>();
   LK_STRACE(6);
 #undef LK_STRACE
+}
+
+// ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------
+//
+// MFMA-bound once N is large, but the activation operand costs 4 B per element (bf16 hi + lo),
+// seven times a Q4_0 weight: a workgroup tile of BM = 256 rows x BN = 64 columns balances the
+// two streams (per CU ~0.8 MB at N 512, K split in two). Eight waves, two per SIMD: four along M
+// x two K-groups (blocks 0-1 / 2-3 of each stage; the groups' sums meet in LDS at the end). A
+// wave owns 64 rows x 64 columns (4 x 4 tiles of v_mfma_f32_16x16x32_bf16): one decoded weight
+// fragment feeds four x-tiles and one activation fragment four row tiles, which keeps both the
+// decode VALU and the LDS reads per MFMA low (all eight waves read the same activations).
+// K runs in stages of 4 blocks through an LDS ring of D stages:
+//   weights: 256 rows x an 80-byte window (the stage's 72 bytes of blocks, rounded up to 16-B
+//            DMA pieces, rows 8-byte aligned), row-major at an 80-B pitch;
+//   activations: the xsplit_kernel fragments of the 4 blocks x 4 x-tiles x (hi, lo), 1 KB each;
+//   Q4_1 only: the 4 blocks' column sums (m·Σx term).
+// Every wave issues the same DMA count per stage (CW), so a counted vmcnt plus one barrier
+// publishes a stage. Q4_0 codes carry their -8 offset ((n - 8)·2^-9, exact), so no T input.
+// Split K: each slice stores an f32 partial slab; splitk_reduce_kernel sums them in order.
+template <int QT> struct WideGeom {
+  static constexpr int NW = 8, KG = 2, MW = NW / KG;             // waves: MW along M x KG K-groups
+  static constexpr int MT = 4, NT = 4;                           // wave tile: 64 rows x 64 columns
+  static constexpr int BM = MW * MT * 16, BN = NT * 16;
+  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr int SB = 4;                                  // blocks per stage
+  static constexpr int WIN = (SB * BB + 15) / 16 * 16;          // weight window bytes per row
+  static constexpr int WPIECES = BM * WIN / 16;                 // 16-B DMA pieces of weights
+  static constexpr int W_INST = (WPIECES + 63) / 64;
+  static constexpr int X_INST = SB * NT * kXSplits;             // 1-KB activation fragments
+  static constexpr int T_INST = (QT == LK_TYPE_Q4_1) ? 1 : 0;
+  static constexpr int CWW = (W_INST + NW - 1) / NW, CWX = (X_INST + NW - 1) / NW, CWT = T_INST;
+  static constexpr int CW = CWW + CWX + CWT;                    // DMA instructions per wave per stage
+  static constexpr int W_BYTES = W_INST * 1024;   // padding instructions (CWW·NW - W_INST) land in DUMMY
+  static constexpr int X_BYTES = X_INST * 1024;
+  static constexpr int T_OFF = W_BYTES + X_BYTES, DUMMY = T_OFF + (T_INST ? 1024 : 0);
+  static constexpr int STAGE = DUMMY + 1024;
+#ifdef LK_WIDE_D
+  static constexpr int D = LK_WIDE_D;
+#else
+  static constexpr int D = (kLdsBytes / STAGE) > 3 ? 3 : (kLdsBytes / STAGE);
+#endif
+  static constexpr int LDS = D * STAGE;
+  static constexpr int OVERREAD = WIN - SB * BB;                // bytes read past a row's last block
+  static_assert(D >= 2, "ring");
+  static_assert((D - 1) * CW < 64, "vmcnt");
+  static_assert(X_INST % NW == 0, "activation pieces per wave");
+  static_assert(SB % KG == 0, "blocks per K-group");
+  static_assert(MW * MT * NT * 256 * 4 <= D * STAGE, "K-group reduction buffer");
+};
+
+struct WideArgs {
+  const uint8_t *a;      // weights (buffer base + dataOffset)
+  const u32x4 *frag;     // xsplit_kernel output (16-column tiles)
+  const float *xsum;     // xsplit_kernel Σx per (block, column) (mult 1 for Q4_1)
+  uint8_t *dst;
+  int64_t d_nb0, d_nb1;
+  float *partial;        // [slices][M][tiles_n·BN] when slices > 1
+  int32_t M, N, K;
+  int32_t tiles_m, tiles_n, slices, kslice;  // kslice: blocks per slice (a multiple of SB)
+  int32_t tasks;                             // task space: super-tiles x sm·sn·slices (grid padded to 8)
+  int32_t sm, sn;                            // super-tile: sm row bands x sn column tiles
+};
+
+template <int QT>
+__global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
+  using G = WideGeom<QT>;
+  constexpr int NW = G::NW, MT = G::MT, NT = G::NT, BM = G::BM, BN = G::BN, BB = G::BB, SB = G::SB, D = G::D;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // Task order (speed only: dispatch is observed round-robin over the 8 XCDs): workgroup b runs
+  // task (b % 8)·(grid / 8) + b / 8, so each XCD gets a contiguous run of tasks; tasks walk
+  // super-tiles of sm row bands x sn column tiles (all slices), so an XCD's L2 holds the
+  // activation fragments of only sn column tiles and the weights of only sm row bands.
+  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+  if (task >= g.tasks) return;  // grid padding
+  const int slice = task % g.slices, u = task / g.slices;
+  const int per_st = g.sm * g.sn, nsn = (g.tiles_n + g.sn - 1) / g.sn;
+  const int st_idx = u / per_st, within = u % per_st;
+  const int tm = (st_idx / nsn) * g.sm + within / g.sn, tn = (st_idx % nsn) * g.sn + within % g.sn;
+  if (tm >= g.tiles_m || tn >= g.tiles_n) return;  // a super-tile past the edge
+  const int nblk = g.K / 32;
+  const int kb0 = slice * g.kslice, kb1 = min(kb0 + g.kslice, nblk);
+  const int nst = (kb1 - kb0) / SB;
+  const int64_t RB = (int64_t)nblk * BB;
+  const int ntx = (g.N + 15) / 16, n16 = ntx * 16;
+
+  // per-lane DMA offsets (fixed for the launch) from each kind's stage base
+  uint32_t wofs[G::CWW], xofs[G::CWX], tofs = 0;
+#pragma unroll
+  for (int c = 0; c < G::CWW; c++) {
+    const int piece = min((wave * G::CWW + c) * 64 + lane, G::WPIECES - 1);
+    const int r = piece / (G::WIN / 16), pc = piece % (G::WIN / 16);
+    const int64_t row = min((int64_t)tm * BM + r, (int64_t)g.M - 1);
+    wofs[c] = (uint32_t)(row * RB + pc * 16);
+  }
+#pragma unroll
+  for (int c = 0; c < G::CWX; c++) {
+    const int x = wave * G::CWX + c;  // (block b, x-tile j, split s)
+    const int b = x / (NT * kXSplits), j = (x / kXSplits) % NT, sp = x % kXSplits;
+    const int xt = min(tn * NT + j, ntx - 1);
+    xofs[c] = (uint32_t)((((int64_t)xt * nblk + b) * kXSplits + sp) * 1024 + lane * 16);
+  }
+  if constexpr (G::T_INST) {
+    const int li = min(lane, SB * BN / 4 - 1);  // lane -> (block li / (BN/4), 4 columns)
+    const int b = li / (BN / 4), c4 = li % (BN / 4);
+    const int n = min(tn * BN + 4 * c4, n16 - 4);
+    tofs = (uint32_t)(((int64_t)b * n16 + n) * 4);
+  }
+  auto issue_stage = [&](int st, int sl) __attribute__((always_inline)) {
+    const int kb = kb0 + min(st, nst - 1) * SB;  // past the last stage: reload the last (never read)
+    const uint8_t *base_a = g.a + (int64_t)kb * BB;
+    const uint8_t *base_x = (const uint8_t *)g.frag + (int64_t)kb * kXSplits * 1024;
+    uint8_t *slot = smem + sl * G::STAGE;
+#pragma unroll
+    for (int c = 0; c < G::CWW; c++) {
+      const int q = wave * G::CWW + c;  // past W_INST: a padding instruction (same count on every wave)
+      dma16<false>(base_a, wofs[c], slot + (q < G::W_INST ? q * 1024 : G::DUMMY));
+    }
+#pragma unroll
+    for (int c = 0; c < G::CWX; c++) dma16<false>(base_x, xofs[c], slot + G::W_BYTES + (wave * G::CWX + c) * 1024);
+    if constexpr (G::T_INST)
+      dma16<false>((const uint8_t *)(g.xsum + (int64_t)kb * n16), tofs, slot + G::T_OFF);
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int mw = wave % G::MW, kg = wave / G::MW;
+  constexpr int BPG = SB / G::KG;  // blocks per K-group per stage
+
+  if (nst > 0) {
+    for (int st = 0; st < D; st++) issue_stage(st, st);
+    int slot = 0;
+    const int m = lane & 15, gq = lane >> 4;
+    for (int st = 0; st < nst; st++) {
+      wait_vmcnt<(D - 1) * G::CW>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const uint8_t *W = smem + slot * G::STAGE;
+      const uint8_t *X = W + G::W_BYTES;
+      const float *T = (const float *)(W + G::T_OFF);
+      // this K-group's blocks of the stage into registers with one burst of LDS reads, so the
+      // slot can be refilled at once and the MFMAs never wait on LDS
+      constexpr int WD = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
+      constexpr bool EARLY = QT != LK_TYPE_Q4_1;  // Q4_1 reads its Σx during the compute
+      uint32_t wd[BPG][MT][WD];
+      u32x4 xh[BPG][NT], xl[BPG][NT];
+#pragma unroll
+      for (int bb = 0; bb < BPG; bb++) {
+        const int b = kg * BPG + bb;
+        const int ob = b * BB;  // kg is wave-uniform: its two parities give two code paths
+#pragma unroll
+        for (int i = 0; i < MT; i++) {
+          const uint8_t *rowp = W + ((mw * MT + i) * 16 + m) * G::WIN;  // window row
+          auto rd = [&](int o) __attribute__((always_inline)) { return *(const uint32_t *)(rowp + o); };
+          if constexpr (QT == LK_TYPE_Q4_1) {
+            wd[bb][i][0] = rd(ob);
+            wd[bb][i][1] = rd(ob + 4 + 4 * gq);
+          } else if constexpr (QT == LK_TYPE_Q4_0) {  // 18-B blocks: ob % 4 == 0 iff b even
+            if ((bb & 1) == 0) {
+              wd[bb][i][0] = rd(ob);
+              wd[bb][i][1] = rd(ob + 4 * gq);
+              wd[bb][i][2] = rd(ob + 4 * gq + 4);
+            } else {
+              wd[bb][i][0] = rd(ob - 2);
+              wd[bb][i][1] = rd(ob + 2 + 4 * gq);
+              wd[bb][i][2] = 0;
+            }
+          } else {  // 34-B blocks: the same parity rule
+            if ((bb & 1) == 0) {
+              wd[bb][i][0] = rd(ob);
+              wd[bb][i][1] = rd(ob + 8 * gq);
+              wd[bb][i][2] = rd(ob + 8 * gq + 4);
+              wd[bb][i][3] = rd(ob + 8 * gq + 8);
+            } else {
+              wd[bb][i][0] = rd(ob - 2);
+              wd[bb][i][1] = rd(ob + 2 + 8 * gq);
+              wd[bb][i][2] = rd(ob + 6 + 8 * gq);
+              wd[bb][i][3] = 0;
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+          const u32x4 *xf = (const u32x4 *)(X + ((b * NT + j) * kXSplits) * 1024) + lane;
+          xh[bb][j] = xf[0];
+          xl[bb][j] = xf[64];
+        }
+      }
+      asm volatile("" ::: "memory");  // the burst stays ahead of the refill
+      if constexpr (EARLY) {
+        wait_lgkmcnt0();
+        __builtin_amdgcn_s_barrier();  // every wave has its copy of this slot: refill it now
+        issue_stage(st + D, slot);
+      }
+#pragma unroll
+      for (int bb = 0; bb < BPG; bb++) {
+        const int b = kg * BPG + bb;
+        bf16x8 wf[MT];
+        float s1[MT], s2[MT];
+#pragma unroll
+        for (int i = 0; i < MT; i++) {
+          s2[i] = 0.f;
+          if constexpr (QT == LK_TYPE_Q4_1) {
+            wf[i] = Q4Frag<0>::make(wd[bb][i][1]);
+            s1[i] = 512.f * h2f(wd[bb][i][0]);
+            s2[i] = h2f(wd[bb][i][0] >> 16);
+          } else if constexpr (QT == LK_TYPE_Q4_0) {
+            if ((bb & 1) == 0) {
+              wf[i] = q4_0_frag_biased(align2(wd[bb][i][2], wd[bb][i][1]));
+              s1[i] = 512.f * h2f(wd[bb][i][0]);
+            } else {
+              wf[i] = q4_0_frag_biased(wd[bb][i][1]);
+              s1[i] = 512.f * h2f(wd[bb][i][0] >> 16);
+            }
+          } else {
+            if ((bb & 1) == 0) {
+              wf[i] = w_frag<LK_TYPE_Q8_0>(align2(wd[bb][i][2], wd[bb][i][1]), align2(wd[bb][i][3], wd[bb][i][2]));
+              s1[i] = h2f(wd[bb][i][0]);
+            } else {
+              wf[i] = w_frag<LK_TYPE_Q8_0>(wd[bb][i][1], wd[bb][i][2]);
+              s1[i] = h2f(wd[bb][i][0] >> 16);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+          f32x4 t = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (QT == LK_TYPE_Q4_1) t = *(const f32x4 *)(T + b * BN + j * 16 + gq * 4);
+#pragma unroll
+          for (int i = 0; i < MT; i++) {
+            f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[bb][j]), wf[i],
+                                                              f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[bb][j]), wf[i], p, 0, 0, 0);
+            accumulate_s<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], p, t);
+          }
+        }
+      }
+      if constexpr (!EARLY) {
+        wait_lgkmcnt0();
+        __builtin_amdgcn_s_barrier();  // every wave is done with this slot
+        issue_stage(st + D, slot);
+      }
+      slot = (slot + 1 == D) ? 0 : slot + 1;
+    }
+    wait_vmcnt<0>();  // drain the padding stages before the ring is reused below
+  }
+  // K-group 1 hands its sums to K-group 0 through LDS (the ring is free now), in a fixed order
+  __syncthreads();
+  f32x4 *red = (f32x4 *)smem + (size_t)mw * (MT * NT * 64) + lane;
+  if (kg == 1) {
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+      for (int j = 0; j < NT; j++) red[(i * NT + j) * 64] = acc[i][j];
+  }
+  __syncthreads();
+  if (kg != 0) return;
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const f32x4 o = red[(i * NT + j) * 64];
+      acc[i][j].x += o.x; acc[i][j].y += o.y; acc[i][j].z += o.z; acc[i][j].w += o.w;
+    }
+  // outputs: lane holds C'(n = 16·(tn·NT + j) + 4(lane>>4) + e, m = tm·BM + (mw·MT + i)·16 + (lane&15))
+  const int npad = g.tiles_n * BN;
+#pragma unroll
+  for (int i = 0; i < MT; i++) {
+    const int64_t m = (int64_t)tm * BM + (mw * MT + i) * 16 + (lane & 15);
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int n0 = tn * BN + j * 16 + 4 * (lane >> 4);
+      if (g.slices > 1) {
+        *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * npad + n0)) = acc[i][j];
+      } else {
+        const float e4[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
+        if (g.d_nb0 == 4 && n0 + 4 <= g.N && ((((uintptr_t)g.dst + m * g.d_nb1 + n0 * 4) & 15) == 0)) {
+          *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = acc[i][j];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+        }
+      }
+    }
+  }
 }
 
 // dst(n, m) = Σ_s P[s][m][n], slices in order (deterministic); one thread per 4 columns.

@@ -361,3 +361,30 @@ def test_skinny_gemm_offsets_strides(gpu, oracle, qt):
         got = gpu_matmul(qt, q, M, K, N, x, **kw)
         ok, msg = parity_ok(got, ref, noise=noise)
         assert ok, (kw, msg)
+
+
+# Wide GEMM (N > 32, K % 128 == 0): 256-row x 64-column tiles, K split over slices when the
+# tiles do not fill the chip, ragged rows / columns, strided outputs.
+WIDE = [
+    (300, 4096, 64),    # split K, ragged rows
+    (257, 1024, 100),   # ragged columns (a 4-column x-tile) and a 1-row tail
+    (64, 11008, 48),    # one row tile, long K
+    (1024, 512, 33),    # the smallest wide N
+]
+
+
+@pytest.mark.parametrize("qt", Q_TYPES, ids=lambda t: QNAME[t])
+@pytest.mark.parametrize("shape", WIDE, ids=lambda s: "x".join(map(str, s)))
+def test_wide_gemm_vs_oracle(gpu, oracle, qt, shape):
+    M, K, N = shape
+    q, x = make_inputs(oracle, qt, M, K, N, seed=M + 3 * N)
+    ref = oracle.mat_mul_q(qt, q, M, K, x, tight=True)
+    noise = noise_for(oracle, qt, q, M, K, x)
+    got = gpu_matmul(qt, q, M, K, N, x)
+    ok, msg = parity_ok(got, ref, noise=noise)
+    assert ok, msg
+    again = gpu_matmul(qt, q, M, K, N, x)
+    assert np.array_equal(got.view(np.uint32), again.view(np.uint32)), "wide GEMM is not deterministic"
+    got = gpu_matmul(qt, q, M, K, N, x, d_off=16, dst_row_pad=5)
+    ok, msg = parity_ok(got, ref, noise=noise)
+    assert ok, ("strided dst", msg)
