@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof}
-ARGS=${BENCH_ARGS:---steps 20 --warmup 5 --no-headline --no-chain --no-batched --no-cpu-baseline}
+ARGS=${BENCH_ARGS:---steps 20 --warmup 5 --no-headline --no-chain --no-batched --no-host-path --no-cpu-baseline}
 mkdir -p "$OUT"
 run() {  # run <name> <secs> <cmd...>
   local name=$1 secs=$2; shift 2
