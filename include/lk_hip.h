@@ -94,6 +94,15 @@ enum lk_status {
 #define LK_Q4_0_BLOCK_BYTES 18
 #define LK_Q4_1_BLOCK_BYTES 20
 #define LK_Q8_0_BLOCK_BYTES 34
+/* K-quants: 256-weight super-blocks (core/GGMLTypes.kt:92-93, :117-122, accessors :734-916).
+ *   Q2_K: scales[16] | qs[64] (2-bit, 4 per byte, low bits first) | f16 d | f16 dmin = 84 B
+ *   Q4_K: f16 d | f16 dmin | scales[12] | qs[128] (low nibble first)       = 144 B
+ *   Q8_K: f32 d | 256 x int8 | 16 x int16 bsums                            = 292 B */
+#define LK_QK_K 256
+#define LK_K_SCALE_SIZE 12
+#define LK_Q2_K_BLOCK_BYTES 84
+#define LK_Q4_K_BLOCK_BYTES 144
+#define LK_Q8_K_BLOCK_BYTES 292
 
 /* A GGMLTensor descriptor (core/GGMLTypes.kt:251-270) as the operator sees it.
  *  - ne/nb: GGMLTensor.ne / GGMLTensor.nb (nb in bytes). Quantized tensors ignore nb,

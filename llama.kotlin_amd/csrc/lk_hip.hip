@@ -85,6 +85,16 @@ int block_bytes(int32_t t) {
   }
 }
 bool is_q(int32_t t) { return block_bytes(t) != 0; }
+// K-quant super-blocks of 256 weights (core/GGMLTypes.kt:117-122)
+int kblock_bytes(int32_t t) {
+  switch (t) {
+    case LK_TYPE_Q2_K: return LK_Q2_K_BLOCK_BYTES;
+    case LK_TYPE_Q4_K: return LK_Q4_K_BLOCK_BYTES;
+    case LK_TYPE_Q8_K: return LK_Q8_K_BLOCK_BYTES;
+    default: return 0;
+  }
+}
+bool is_kq(int32_t t) { return kblock_bytes(t) != 0; }
 
 // rank / numElements (core/GGMLTypes.kt:275-300), used by getNumBlocks' bound.
 int t_rank(const lk_tensor *t) {
@@ -120,7 +130,7 @@ void span2(const lk_tensor *t, int64_t n0, int64_t n1, uint64_t width, uint64_t 
   *hi = t->data_offset + (uint64_t)(n0 - 1) * t->nb[0] + (uint64_t)(n1 - 1) * t->nb[1] + width;
 }
 
-enum class Path { kQuantF32, kF32, kF16 };
+enum class Path { kQuantF32, kKQuantF32, kF32, kF16 };
 
 struct Checked {
   Path path;
@@ -148,8 +158,10 @@ int check(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, Checked 
     if (dst->type != LK_TYPE_F32) /* :1449, :1463, :1517 */
       return fail(LK_ERR_INVALID_ARG, "Result tensor type must be F32 for quantized x F32 matmul");
     c->path = Path::kQuantF32;
-  } else if (b->type == LK_TYPE_F32 && (a->type == LK_TYPE_Q2_K || a->type == LK_TYPE_Q4_K || a->type == LK_TYPE_Q8_K)) {
-    return fail(LK_ERR_NOT_IMPLEMENTED, "K-quant x F32 is not offloaded (CPU path)");
+  } else if (is_kq(a->type) && b->type == LK_TYPE_F32) {
+    if (dst->type != LK_TYPE_F32) /* :1484, :1495, :1506 */
+      return fail(LK_ERR_INVALID_ARG, "Result tensor type must be F32 for K-quant x F32 matmul");
+    c->path = Path::kKQuantF32;
   } else {
     if (dst->type != a->type) /* :1530 */
       return fail(LK_ERR_INVALID_ARG, "Result tensor type must match first input type for general matmul");
@@ -179,6 +191,18 @@ int check(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, Checked 
       c->a_hi = a->data_offset + (uint64_t)(last_blk + 1) * block_bytes(a->type);
       if (c->a_hi > a->buf_bytes)
         return fail(LK_ERR_OUT_OF_BOUNDS, "quant block read ends at %llu, out of buffer bounds %llu",
+                    (unsigned long long)c->a_hi, (unsigned long long)a->buf_bytes);
+    } else if (c->path == Path::kKQuantF32) {
+      // getNumBlocks = numElements / 256 (core/GGMLTypes.kt:518); the partial path reads the
+      // block of flat index M*K-1; full blocks never reach past it
+      const int64_t last_blk = (M * K - 1) / 256;
+      const int64_t nblk = t_num_elements(a) / 256;
+      if (last_blk >= nblk)
+        return fail(LK_ERR_INVALID_ARG, "blockIndex %lld out of bounds for %lld blocks", (long long)last_blk, (long long)nblk);
+      c->a_lo = a->data_offset;
+      c->a_hi = a->data_offset + (uint64_t)(last_blk + 1) * kblock_bytes(a->type);
+      if (c->a_hi > a->buf_bytes)
+        return fail(LK_ERR_OUT_OF_BOUNDS, "K-quant block read ends at %llu, out of buffer bounds %llu",
                     (unsigned long long)c->a_hi, (unsigned long long)a->buf_bytes);
     } else {
       span2(a, K, M, ew, &c->a_lo, &c->a_hi);
@@ -634,6 +658,27 @@ int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const
   return LK_OK;
 }
 
+// K-quant x F32: one wave per output (kquant_mul_mat_kernel).
+int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  KQuantArgs g{};
+  g.a = (const uint8_t *)a->data + a->data_offset;
+  g.b = (const uint8_t *)b->data + b->data_offset;
+  g.dst = (uint8_t *)dst->data + dst->data_offset;
+  g.b_nb0 = b->nb[0]; g.b_nb1 = b->nb[1]; g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
+  g.M = c.M; g.N = c.N; g.K = c.K;
+  const int64_t blocks = (c.M * c.N + 3) / 4;
+  if (blocks > (int64_t)INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "output too large for the K-quant kernel");
+  dim3 grid((unsigned)blocks), block(256);
+  switch (a->type) {
+    case LK_TYPE_Q2_K: hipLaunchKernelGGL(kquant_mul_mat_kernel<LK_TYPE_Q2_K>, grid, block, 0, st, g); break;
+    case LK_TYPE_Q4_K: hipLaunchKernelGGL(kquant_mul_mat_kernel<LK_TYPE_Q4_K>, grid, block, 0, st, g); break;
+    case LK_TYPE_Q8_K: hipLaunchKernelGGL(kquant_mul_mat_kernel<LK_TYPE_Q8_K>, grid, block, 0, st, g); break;
+    default: return fail(LK_ERR_NOT_IMPLEMENTED, "K-quant: type %d", a->type);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
 // Single eligible GEMV: the descriptor travels in the kernel arguments (no
 // allocation, no host sync: stream-ordered and graph-capturable).
 int run_single_gemv(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
@@ -652,6 +697,7 @@ int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *ds
     }
     return launch_generic(a, b, dst, c, st);
   }
+  if (c.path == Path::kKQuantF32) return launch_kquant(a, b, dst, c, st);
   if (gemv_eligible(a, b, dst, c)) return run_single_gemv(a, b, dst, c, st);
   if (gemm_eligible(c)) return skinny_eligible(a, c) ? launch_skinny(a, b, dst, c, st) : launch_gemm(a, b, dst, c, st);
   return launch_generic(a, b, dst, c, st);
@@ -791,6 +837,7 @@ int lk_weights_pin(const lk_tensor *a, uint64_t generation) {
   if (!a || !a->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
   uint64_t bytes;
   if (is_q(a->type)) bytes = (uint64_t)(t_num_elements(a) / 32) * block_bytes(a->type);
+  else if (is_kq(a->type)) bytes = (uint64_t)(t_num_elements(a) / 256) * kblock_bytes(a->type);
   else bytes = (uint64_t)t_num_elements(a) * (a->type == LK_TYPE_F16 ? 2 : 4);
   if (a->data_offset + bytes > a->buf_bytes) return fail(LK_ERR_OUT_OF_BOUNDS, "pin: tensor exceeds its buffer");
   return pin_on(cur(), a, a->data_offset, bytes, generation);

@@ -1785,6 +1785,97 @@ __global__ __launch_bounds__(256) void mul_mat_generic_kernel(GenericArgs g) {
   }
 }
 
+// ---- K-quant dots: Q2_K / Q4_K / Q8_K x F32 (core/GGMLComputeOps.kt:152-432) -------------------
+//
+// llama.kotlin's own K-quant formulas (not upstream ggml's), element for element: every weight
+// is the value the Kotlin loop computes for (row, k) — f32 roundings in the same order, no
+// contraction — including its "full block" reading of block (row·K + blockStart)/256 from item 0
+// when K % 256 != 0 and the flat-index partial path with its own formula (Q4_K adds dmin there).
+// Only the order of the f32 sum differs. One wave per output (i, j): lane l takes the 4
+// consecutive k = 256·s + 4l .. +3 of every 256-span s (one sub-block, so one scale/min).
+
+struct KQuantArgs {
+  const uint8_t *a;            // blocks (buffer base + dataOffset)
+  const uint8_t *b;            // B(n, k) at n·b_nb0 + k·b_nb1
+  uint8_t *dst;                // dst(n, m) at n·d_nb0 + m·d_nb1
+  int64_t b_nb0, b_nb1, d_nb0, d_nb1;
+  int64_t M, N, K;
+};
+
+template <int QT> struct KQTraits;
+template <> struct KQTraits<LK_TYPE_Q2_K> { static constexpr int BB = LK_Q2_K_BLOCK_BYTES; };
+template <> struct KQTraits<LK_TYPE_Q4_K> { static constexpr int BB = LK_Q4_K_BLOCK_BYTES; };
+template <> struct KQTraits<LK_TYPE_Q8_K> { static constexpr int BB = LK_Q8_K_BLOCK_BYTES; };
+
+__device__ __forceinline__ int sbyte(const uint8_t *p) { return (int)(int8_t)*p; }  // Kotlin Byte.toInt()
+__device__ __forceinline__ float kq_h(const uint8_t *p) { return h2f((uint32_t)p[0] | ((uint32_t)p[1] << 8)); }
+
+// The weight of item `item` of block `blk`; FULL selects the full-block formulas.
+template <int QT, bool FULL>
+__device__ __forceinline__ float kq_weight(const uint8_t *blk, int item) {
+  if constexpr (QT == LK_TYPE_Q2_K) {  // :182-196 (full), :216-227 (partial): the same formulas
+    const float d = kq_h(blk + 80), dmin = kq_h(blk + 82);
+    const int sb = item / 16;
+    const int sm = sbyte(blk + sb);
+    const float scale = __fmul_rn(__fdiv_rn((float)(sm & 0x0F), 15.0f), d);
+    const float mn = __fadd_rn(__fmul_rn((float)((sm >> 4) & 0x0F), d), dmin);
+    const int qb = sbyte(blk + 16 + sb * 4 + (item % 16) / 4);
+    const int q = (qb >> (((item % 16) % 4) * 2)) & 0x03;
+    return __fadd_rn(__fmul_rn(__fdiv_rn((float)q, 3.0f), scale), mn);
+  } else if constexpr (QT == LK_TYPE_Q4_K) {
+    const float d = kq_h(blk), dmin = kq_h(blk + 2);
+    const int sb = item / 32;
+    const int sc = sbyte(blk + 4 + sb);
+    const float scale = __fmul_rn(__fdiv_rn((float)(sc & 0x3F), 63.0f), d);
+    const int qb = sbyte(blk + 4 + LK_K_SCALE_SIZE + sb * 16 + (item % 32) / 2);
+    const int q = (item % 2 == 0) ? (qb & 0x0F) : ((qb >> 4) & 0x0F);
+    float off;
+    if constexpr (FULL) {  // :274-287: 6-bit min from the scale byte's top bits + a nibble of byte 4 + 2sb + 1
+      const int qmh = (sb * 2 + 1 < LK_K_SCALE_SIZE) ? (sbyte(blk + 4 + sb * 2 + 1) & 0x0F) : 0;
+      const int qm = ((sc >> 6) & 0x03) | (qmh << 2);
+      off = __fadd_rn(__fmul_rn(__fdiv_rn((float)qm, 63.0f), d), dmin);
+    } else {               // :331: the partial path adds dmin itself
+      off = dmin;
+    }
+    return __fadd_rn(__fmul_rn(__fdiv_rn((float)q, 15.0f), scale), off);
+  } else {  // Q8_K :404-407, :418-420
+    const float d = __builtin_bit_cast(float, (uint32_t)blk[0] | ((uint32_t)blk[1] << 8) | ((uint32_t)blk[2] << 16) |
+                                                  ((uint32_t)blk[3] << 24));
+    return __fmul_rn((float)sbyte(blk + 4 + item), d);
+  }
+}
+
+template <int QT>
+__global__ __launch_bounds__(256) void kquant_mul_mat_kernel(KQuantArgs g) {
+  constexpr int BB = KQTraits<QT>::BB;
+  const int64_t out = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (out >= g.M * g.N) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = out / g.N, j = out % g.N;
+  const uint8_t *xb = g.b + j * g.b_nb0;
+  float s = 0.f;
+  for (int64_t bs = 0; bs < g.K; bs += LK_QK_K) {
+    const int64_t be = min(bs + (int64_t)LK_QK_K, g.K);
+    if (be - bs == LK_QK_K) {
+      const uint8_t *blk = g.a + ((i * g.K + bs) / LK_QK_K) * BB;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int item = 4 * lane + e;
+        const float w = kq_weight<QT, true>(blk, item);
+        s = fmaf(w, *(const float *)(xb + (bs + item) * g.b_nb1), s);
+      }
+    } else {
+      for (int64_t k = bs + lane; k < be; k += 64) {
+        const int64_t flat = i * g.K + k;
+        const float w = kq_weight<QT, false>(g.a + (flat / LK_QK_K) * BB, (int)(flat % LK_QK_K));
+        s = fmaf(w, *(const float *)(xb + k * g.b_nb1), s);
+      }
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) *(float *)(g.dst + j * g.d_nb0 + i * g.d_nb1) = s;
+}
+
 // ---- format kernels (dequantizeTensor / quantizeTensor) -------------------------
 
 // dequantizeTensor (GGMLComputeOps.kt:918-964): one thread per block, bit-exact

@@ -142,7 +142,7 @@ class GGMLHipBackend:
         a, b = tensor.src[0], tensor.src[1]
         if a is None or b is None:
             return False
-        if a.type in (GGMLType.Q4_0, GGMLType.Q4_1, GGMLType.Q8_0):
+        if a.type in (GGMLType.Q4_0, GGMLType.Q4_1, GGMLType.Q8_0, GGMLType.Q2_K, GGMLType.Q4_K, GGMLType.Q8_K):
             return b.type == GGMLType.F32 and tensor.type == GGMLType.F32
         if a.type == GGMLType.F32:
             return b.type == GGMLType.F32 and tensor.type == GGMLType.F32

@@ -102,7 +102,8 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) :
         if (tensor.op != GGMLOp.MUL_MAT) return false
         val a = tensor.src[0] ?: return false
         val b = tensor.src[1] ?: return false
-        val quant = (a.type == GGMLType.Q4_0 || a.type == GGMLType.Q4_1 || a.type == GGMLType.Q8_0) &&
+        val quant = (a.type == GGMLType.Q4_0 || a.type == GGMLType.Q4_1 || a.type == GGMLType.Q8_0 ||
+            a.type == GGMLType.Q2_K || a.type == GGMLType.Q4_K || a.type == GGMLType.Q8_K) &&
             b.type == GGMLType.F32 && tensor.type == GGMLType.F32
         val general = (a.type == GGMLType.F32 && b.type == GGMLType.F32 && tensor.type == GGMLType.F32) ||
             (a.type == GGMLType.F16 && b.type == GGMLType.F16 && tensor.type == GGMLType.F16)

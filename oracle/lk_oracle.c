@@ -163,6 +163,9 @@ int lko_block_bytes(int32_t type) { /* core/GGMLTypes.kt:99-114 */
     case LK_TYPE_Q4_0: return LK_Q4_0_BLOCK_BYTES;
     case LK_TYPE_Q4_1: return LK_Q4_1_BLOCK_BYTES;
     case LK_TYPE_Q8_0: return LK_Q8_0_BLOCK_BYTES;
+    case LK_TYPE_Q2_K: return LK_Q2_K_BLOCK_BYTES; /* :117 */
+    case LK_TYPE_Q4_K: return LK_Q4_K_BLOCK_BYTES; /* :119 */
+    case LK_TYPE_Q8_K: return LK_Q8_K_BLOCK_BYTES; /* :122 */
     default: return 0;
   }
 }
@@ -203,6 +206,7 @@ static int64_t t_num_blocks(const lk_tensor *t) {
   int64_t total = t_num_elements(t);
   if (total == 0) return 0;
   if (t->type == LK_TYPE_Q4_0 || t->type == LK_TYPE_Q4_1 || t->type == LK_TYPE_Q8_0) return total / 32;
+  if (t->type == LK_TYPE_Q2_K || t->type == LK_TYPE_Q4_K || t->type == LK_TYPE_Q8_K) return total / LK_QK_K; /* :518 */
   return 0;
 }
 
@@ -450,6 +454,210 @@ static float dot_q80_f32(const lk_tensor *a, const lk_tensor *b, int64_t row, in
   return sum;
 }
 
+
+/* ---- K-quants (core/GGMLComputeOps.kt:152-432, core/GGMLTypes.kt:734-916) ----------------
+ * Block layouts (llama.kotlin's, core/GGMLTypes.kt:117-122 and the accessors):
+ *   Q2_K (84 B):  scales[16] | qs[64] | d f16 @80 | dmin f16 @82
+ *   Q4_K (144 B): d f16 @0 | dmin f16 @2 | scales[12] @4 | qs[128] @16
+ *   Q8_K (292 B): d f32 @0 | qs[256] int8 @4 | bsums[16] int16 @260 (not read)
+ * The "full block" paths take blockIndex = (row*K + blockStart) / 256 and read its items
+ * 0..255 for k = blockStart..blockStart+255, also when K % 256 != 0 (then that block does not
+ * start at the row's k = blockStart); the trailing partial block goes element by element
+ * through the flat index, with its own formulas (Q4_K's partial path adds dmin, not min). */
+
+/* raw buffer byte (buffer[offset], Kotlin ByteArray index: AIOOBE past the end) */
+static int raw_byte(const lk_tensor *t, uint64_t off, int *st) {
+  if (t->data == NULL) { *st = fail(LK_ERR_NO_BUFFER, "Tensor buffer not found"); return 0; }
+  if (off >= t->buf_bytes) { *st = fail(LK_ERR_OUT_OF_BOUNDS, "buffer index %llu out of bounds", (unsigned long long)off); return 0; }
+  *st = LK_OK;
+  return (int)(int8_t)((const uint8_t *)t->data)[off]; /* Byte: signed */
+}
+/* getQ2_KBlockScale :740-752 (d @ 16+64), getQ2_KBlockScaleMin :757-769 (dmin @ 82) */
+static float q2k_d(const lk_tensor *t, int64_t blk, uint64_t inner, int *st) {
+  const uint8_t *p = block_byte(t, LK_TYPE_Q2_K, blk, inner, 2, st);
+  return p ? lko_half_to_float(rd_u16(p)) : 0.0f;
+}
+/* getQ2_KScale :774-783 / getQ2_KQuant :788-797: index range only, then buffer[...] */
+static int q2k_byte(const lk_tensor *t, int64_t blk, uint64_t inner, int *st) {
+  return raw_byte(t, t->data_offset + (uint64_t)blk * LK_Q2_K_BLOCK_BYTES + inner, st);
+}
+/* getQ4_KBlockScale :822-833 (d @ 0), getQ4_KBlockScaleMin :838-849 (dmin @ 2) */
+static float q4k_d(const lk_tensor *t, int64_t blk, uint64_t inner, int *st) {
+  const uint8_t *p = block_byte(t, LK_TYPE_Q4_K, blk, inner, 2, st);
+  return p ? lko_half_to_float(rd_u16(p)) : 0.0f;
+}
+/* getQ8_KBlockScale :881-894 (getFloatLe @ 0), getQ8_KWeight :903-916 */
+static float q8k_d(const lk_tensor *t, int64_t blk, int *st) {
+  const uint8_t *p = block_byte(t, LK_TYPE_Q8_K, blk, 0, 4, st);
+  return p ? rd_f32(p) : 0.0f;
+}
+static int32_t q8k_weight(const lk_tensor *t, int64_t blk, int32_t item, int *st) {
+  const uint8_t *p = block_byte(t, LK_TYPE_Q8_K, blk, 4 + (uint64_t)item, 1, st);
+  return p ? (int32_t)(int8_t)p[0] : 0;
+}
+
+/* Q2_K scale/min of sub-block sb: (qs/15)*d, qm*d + dmin — :182-187 */
+static void q2k_scale_min(int sm, float d, float dmin, float *scale, float *min) {
+  const int32_t qs = sm & 0x0F, qm = kushr(sm, 4) & 0x0F; /* shr on the sign-extended byte, & 0x0F */
+  const float r = (float)qs / 15.0f;
+  *scale = r * d;
+  const float md = (float)qm * d;
+  *min = md + dmin;
+}
+/* (q/3)*scale + min — :196, :227 */
+static float q2k_value(int32_t q, float scale, float min) {
+  const float r = (float)q / 3.0f;
+  const float t = r * scale;
+  return t + min;
+}
+
+/* computeDotProductQ2_KF32 — :152-234 */
+static float dot_q2k_f32(const lk_tensor *a, const lk_tensor *b, int64_t row, int64_t col, int64_t K, int *st) {
+  float sum = 0.0f;
+  for (int64_t bs = 0; bs < K; bs += LK_QK_K) {
+    const int64_t be = bs + LK_QK_K < K ? bs + LK_QK_K : K;
+    if (be - bs == LK_QK_K) {
+      const int64_t blk = (row * K + bs) / LK_QK_K;
+      const float d = q2k_d(a, blk, 80, st); if (*st) return 0;
+      const float dmin = q2k_d(a, blk, 82, st); if (*st) return 0;
+      for (int sb = 0; sb < LK_QK_K / 16; sb++) {
+        const int sm = q2k_byte(a, blk, (uint64_t)sb, st); if (*st) return 0;
+        float scale, min;
+        q2k_scale_min(sm, d, dmin, &scale, &min);
+        for (int i = 0; i < 16; i += 4) {
+          const int qb = q2k_byte(a, blk, 16 + (uint64_t)(sb * 4 + i / 4), st); if (*st) return 0;
+          for (int j = 0; j < 4; j++) {
+            const int64_t k = bs + sb * 16 + i + j;
+            if (k < be) {
+              const int32_t q = kushr(qb, j * 2) & 0x03; /* qb >> 2j on the sign-extended byte */
+              const float w = q2k_value(q, scale, min);
+              const float x = get_float(b, col, k, st); if (*st) return 0;
+              const float p = w * x;
+              sum = sum + p;
+            }
+          }
+        }
+      }
+    } else {
+      for (int64_t k = bs; k < be; k++) {
+        const int64_t flat = row * K + k, blk = flat / LK_QK_K;
+        const int32_t item = (int32_t)(flat % LK_QK_K);
+        const float d = q2k_d(a, blk, 80, st); if (*st) return 0;
+        const float dmin = q2k_d(a, blk, 82, st); if (*st) return 0;
+        const int sb = item / 16;
+        const int sm = q2k_byte(a, blk, (uint64_t)sb, st); if (*st) return 0;
+        float scale, min;
+        q2k_scale_min(sm, d, dmin, &scale, &min);
+        const int qb = q2k_byte(a, blk, 16 + (uint64_t)(sb * 4 + (item % 16) / 4), st); if (*st) return 0;
+        const int32_t q = kushr(qb, ((item % 16) % 4) * 2) & 0x03;
+        const float w = q2k_value(q, scale, min);
+        const float x = get_float(b, col, k, st); if (*st) return 0;
+        const float p = w * x;
+        sum = sum + p;
+      }
+    }
+  }
+  return sum;
+}
+
+/* (q/15)*scale + off — :297-306, :331 */
+static float q4k_value(int32_t q, float scale, float off) {
+  const float r = (float)q / 15.0f;
+  const float t = r * scale;
+  return t + off;
+}
+
+/* computeDotProductQ4_KF32 — :241-339 */
+static float dot_q4k_f32(const lk_tensor *a, const lk_tensor *b, int64_t row, int64_t col, int64_t K, int *st) {
+  float sum = 0.0f;
+  for (int64_t bs = 0; bs < K; bs += LK_QK_K) {
+    const int64_t be = bs + LK_QK_K < K ? bs + LK_QK_K : K;
+    if (be - bs == LK_QK_K) {
+      const int64_t blk = (row * K + bs) / LK_QK_K;
+      const float d = q4k_d(a, blk, 0, st); if (*st) return 0;
+      const float dmin = q4k_d(a, blk, 2, st); if (*st) return 0;
+      const uint64_t bo = a->data_offset + (uint64_t)blk * LK_Q4_K_BLOCK_BYTES;
+      for (int sb = 0; sb < 8; sb++) {
+        const int sc = raw_byte(a, bo + 4 + (uint64_t)sb, st); if (*st) return 0;
+        const int32_t qs = sc & 0x3F, qml = kushr(sc, 6) & 0x03;
+        int32_t qmh = 0;
+        if (sb * 2 + 1 < LK_K_SCALE_SIZE) { qmh = raw_byte(a, bo + 4 + (uint64_t)(sb * 2 + 1), st) & 0x0F; if (*st) return 0; }
+        const int32_t qm = qml | kshl(qmh, 2);
+        const float scale = ((float)qs / 63.0f) * d;
+        const float mr = (float)qm / 63.0f;
+        const float mt = mr * d;
+        const float min = mt + dmin;
+        const uint64_t qo = bo + 4 + LK_K_SCALE_SIZE + (uint64_t)sb * 16;
+        for (int i = 0; i < 32; i += 2) {
+          const int64_t k1 = bs + sb * 32 + i, k2 = k1 + 1;
+          if (k1 < be) {
+            const int qb = raw_byte(a, qo + (uint64_t)(i / 2), st); if (*st) return 0;
+            const float w1 = q4k_value(qb & 0x0F, scale, min);
+            const float x1 = get_float(b, col, k1, st); if (*st) return 0;
+            const float p1 = w1 * x1;
+            sum = sum + p1;
+            if (k2 < be) {
+              const float w2 = q4k_value(kushr(qb, 4) & 0x0F, scale, min);
+              const float x2 = get_float(b, col, k2, st); if (*st) return 0;
+              const float p2 = w2 * x2;
+              sum = sum + p2;
+            }
+          }
+        }
+      }
+    } else {
+      for (int64_t k = bs; k < be; k++) {
+        const int64_t flat = row * K + k, blk = flat / LK_QK_K;
+        const int32_t item = (int32_t)(flat % LK_QK_K);
+        const float d = q4k_d(a, blk, 0, st); if (*st) return 0;
+        const float dmin = q4k_d(a, blk, 2, st); if (*st) return 0;
+        const int sb = item / 32;
+        const uint64_t bo = a->data_offset + (uint64_t)blk * LK_Q4_K_BLOCK_BYTES;
+        const int sc = raw_byte(a, bo + 4 + (uint64_t)sb, st); if (*st) return 0;
+        const float scale = ((float)(sc & 0x3F) / 63.0f) * d;
+        const int qb = raw_byte(a, bo + 4 + LK_K_SCALE_SIZE + (uint64_t)sb * 16 + (uint64_t)((item % 32) / 2), st); if (*st) return 0;
+        const int32_t q = ((item % 32) % 2 == 0) ? (qb & 0x0F) : (kushr(qb, 4) & 0x0F);
+        const float w = q4k_value(q, scale, dmin);
+        const float x = get_float(b, col, k, st); if (*st) return 0;
+        const float p = w * x;
+        sum = sum + p;
+      }
+    }
+  }
+  return sum;
+}
+
+/* computeDotProductQ8_KF32 — :385-432 */
+static float dot_q8k_f32(const lk_tensor *a, const lk_tensor *b, int64_t row, int64_t col, int64_t K, int *st) {
+  float sum = 0.0f;
+  for (int64_t bs = 0; bs < K; bs += LK_QK_K) {
+    const int64_t be = bs + LK_QK_K < K ? bs + LK_QK_K : K;
+    if (be - bs == LK_QK_K) {
+      const int64_t blk = (row * K + bs) / LK_QK_K;
+      const float d = q8k_d(a, blk, st); if (*st) return 0;
+      for (int i = 0; i < LK_QK_K; i++) {
+        const int32_t q = q8k_weight(a, blk, i, st); if (*st) return 0;
+        const float w = (float)q * d;
+        const float x = get_float(b, col, bs + i, st); if (*st) return 0;
+        const float p = w * x;
+        sum = sum + p;
+      }
+    } else {
+      for (int64_t k = bs; k < be; k++) {
+        const int64_t flat = row * K + k, blk = flat / LK_QK_K;
+        const int32_t item = (int32_t)(flat % LK_QK_K);
+        const float d = q8k_d(a, blk, st); if (*st) return 0;
+        const int32_t q = q8k_weight(a, blk, item, st); if (*st) return 0;
+        const float w = (float)q * d;
+        const float x = get_float(b, col, k, st); if (*st) return 0;
+        const float p = w * x;
+        sum = sum + p;
+      }
+    }
+  }
+  return sum;
+}
+
 /* Error replay of dequantizeTensor(t) (:918-964) for the dead fallbacks: it
  * reads every element through the accessors, so its errors surface first. */
 static int dequant_errors(const lk_tensor *t) {
@@ -495,7 +703,20 @@ int lko_compute_mat_mul(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) 
     return LK_OK;
   }
   if (b->type == LK_TYPE_F32 && (a->type == LK_TYPE_Q2_K || a->type == LK_TYPE_Q4_K || a->type == LK_TYPE_Q8_K)) {
-    return fail(LK_ERR_NOT_IMPLEMENTED, "K-quant x F32 (:1483-1514) is outside this restatement's scope");
+    /* :1483-1514 */
+    if (dst->type != LK_TYPE_F32) return fail(LK_ERR_INVALID_ARG, "Result tensor type must be F32 for K-quant x F32 matmul");
+    for (int64_t i = 0; i < M; i++) {
+      for (int64_t j = 0; j < N; j++) {
+        float r;
+        if (a->type == LK_TYPE_Q2_K) r = dot_q2k_f32(a, b, i, j, K, &st);
+        else if (a->type == LK_TYPE_Q4_K) r = dot_q4k_f32(a, b, i, j, K, &st);
+        else r = dot_q8k_f32(a, b, i, j, K, &st);
+        if (st) return st;
+        set_float(dst, r, j, i, &st);
+        if (st) return st;
+      }
+    }
+    return LK_OK;
   }
   /* general fallback :1530-1564 */
   if (dst->type != a->type) return fail(LK_ERR_INVALID_ARG, "Result tensor type must match first input type for general matmul");

@@ -24,8 +24,9 @@ LIB_PATH = os.path.join(HERE, "build", "liblk_oracle.so")
 # lk_type ids (include/lk_hip.h; GGMLType.fromValue, core/GGMLTypes.kt:145-168)
 F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0 = 0, 1, 2, 3, 4, 5, 6
 Q2_K, Q4_K, Q8_K, I8, I16, I32, I64 = 8, 10, 13, 15, 16, 17, 18
-BLOCK_BYTES = {Q4_0: 18, Q4_1: 20, Q8_0: 34}
-TYPE_NAMES = {F32: "F32", F16: "F16", Q4_0: "Q4_0", Q4_1: "Q4_1", Q8_0: "Q8_0"}
+BLOCK_BYTES = {Q4_0: 18, Q4_1: 20, Q8_0: 34, Q2_K: 84, Q4_K: 144, Q8_K: 292}
+QK_K = 256
+TYPE_NAMES = {F32: "F32", F16: "F16", Q4_0: "Q4_0", Q4_1: "Q4_1", Q8_0: "Q8_0", Q2_K: "Q2_K", Q4_K: "Q4_K", Q8_K: "Q8_K"}
 
 
 class LkTensor(ctypes.Structure):

@@ -1,0 +1,90 @@
+"""K-quant dots Q2_K / Q4_K / Q8_K x F32 (core/GGMLComputeOps.kt:152-432,
+dispatched at :1483-1514).
+
+Pinning: the reference has no known-answer test for these dots (its K-quant tests cover
+quantize/dequantize accuracy only, T/core/GGMLKQuantAccuracyTest.kt), so the C oracle is
+cross-checked against an independent Python restatement (tests/_kquant.py) on random
+super-blocks: bit-exact, since both accumulate left to right in f32 — parity with the
+reference itself is unpinned. The GPU path must match the oracle within the §8c F32 bar."""
+import numpy as np
+import pytest
+
+import oracle as O
+from _kquant import BB, Q2_K, Q4_K, Q8_K, mat_mul_kq_ref, random_kblocks
+from _util import parity_ok, random_acts
+
+KQ = [Q2_K, Q4_K, Q8_K]
+KNAME = {Q2_K: "Q2_K", Q4_K: "Q4_K", Q8_K: "Q8_K"}
+# K % 256 != 0 exercises the full-block quirk (rows after the first read a block that does not
+# start at their k) and the flat-index partial path
+SMALL = [(4, 256, 1), (3, 512, 2), (8, 320, 1), (2, 768, 3), (16, 64, 1)]
+
+
+def _x(K, N, seed):
+    return random_acts(K * N, seed).reshape(K, N)
+
+
+@pytest.mark.parametrize("qt", KQ, ids=lambda t: KNAME[t])
+@pytest.mark.parametrize("shape", SMALL, ids=lambda s: "x".join(map(str, s)))
+def test_oracle_matches_python_restatement(qt, shape):
+    M, K, N = shape
+    raw = random_kblocks(qt, M * K // 256, seed=M * 7 + K)
+    x = _x(K, N, 3 + M)
+    got = O.mat_mul_q(qt, raw, M, K, x)
+    ref = mat_mul_kq_ref(qt, raw, M, K, x)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("qt", KQ, ids=lambda t: KNAME[t])
+def test_oracle_block_bound_and_dst_type(qt):
+    # M*K % 256 != 0: the partial path reaches block numBlocks -> IllegalArgumentException
+    raw = random_kblocks(qt, 2, seed=1)
+    with pytest.raises(O.OracleError) as e:
+        O.mat_mul_q(qt, np.concatenate([raw, np.zeros(BB[qt], np.uint8)]), 3, 200, _x(200, 1, 1))
+    assert e.value.status == 1
+    a = O.make_tensor(qt, [256, 1], random_kblocks(qt, 1, 2))
+    b = O.make_tensor(O.F32, [1, 256], _x(256, 1, 2).view(np.uint8).reshape(-1))
+    d = O.make_tensor(O.F16, [1, 1], np.zeros(2, np.uint8))
+    assert O.compute_mat_mul(a, b, d) == 1
+
+
+GPU_SHAPES = SMALL + [(257, 4096, 1), (64, 11008, 2), (100, 4096, 4)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("qt", KQ, ids=lambda t: KNAME[t])
+@pytest.mark.parametrize("shape", GPU_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_kquant_gpu_vs_oracle(gpu, qt, shape):
+    from test_gpu_parity import gpu_matmul
+    M, K, N = shape
+    raw = random_kblocks(qt, M * K // 256, seed=M + K + N)
+    x = _x(K, N, 11 + N)
+    ref = O.mat_mul_q(qt, raw, M, K, x)
+    got = gpu_matmul(qt, raw, M, K, N, x)
+    ok, msg = parity_ok(got, ref)
+    assert ok, msg
+    got = gpu_matmul(qt, raw, M, K, N, x, host=True, dst_row_pad=2)
+    ok, msg = parity_ok(got, ref)
+    assert ok, ("host path", msg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("qt", KQ, ids=lambda t: KNAME[t])
+def test_kquant_gpu_errors_like_oracle(gpu, qt):
+    import ggml_hip as G
+    raw = np.concatenate([random_kblocks(qt, 2, seed=5), np.zeros(BB[qt], np.uint8)])
+    ga = G.GGMLGraphAllocator(device="cuda", defaultBufferSize=16)
+    ia, ib, idd = ga.addBuffer(raw.size + 64), ga.addBuffer(4 * 200 + 64), ga.addBuffer(64)
+    a = G.GGMLTensor(G.GGMLType(qt), [200, 3], bufferId=ia)
+    b = G.GGMLTensor(G.GGMLType.F32, [1, 200], bufferId=ib)
+    d = G.GGMLTensor(G.GGMLType.F32, [1, 3], bufferId=idd)
+    ga.setTensorBytes(a, raw)
+    with pytest.raises(G.IllegalArgumentException):  # M*K % 256 != 0: block numBlocks is read
+        G.computeMatMul(ga, ga.context, a, b, d)
+    a2 = G.GGMLTensor(G.GGMLType(qt), [256, 1], bufferId=ia)
+    b2 = G.GGMLTensor(G.GGMLType.F32, [1, 256], bufferId=ga.addBuffer(4 * 256))
+    with pytest.raises(G.IllegalArgumentException):  # dst must be F32 (:1484, :1495, :1506)
+        G.computeMatMul(ga, ga.context, a2, b2, G.GGMLTensor(G.GGMLType.F16, [1, 1], bufferId=idd))
+    short = G.GGMLTensor(G.GGMLType(qt), [256, 1], bufferId=ga.addBuffer(BB[qt] - 4))
+    with pytest.raises(G.IndexOutOfBoundsException):  # the block runs past the buffer
+        G.computeMatMul(ga, ga.context, short, b2, G.GGMLTensor(G.GGMLType.F32, [1, 1], bufferId=idd))
