@@ -399,10 +399,12 @@ __device__ __forceinline__ float dpp_sum(float v) {
 // (100 MHz) at kernel entry, activations in VGPRs, first unit decoded, and exit.
 #ifdef LK_STREAM_TRACE
 __device__ uint64_t *lk_trace_buf;
+// the buffer pointer comes from a scalar load (a vector load would wait behind the DMA)
 #define LK_TRACE(slot)                                                                                  \
   do {                                                                                                  \
-    if (lane == 0 && lk_trace_buf)                                                                      \
-      lk_trace_buf[((size_t)blockIdx.x * kStreamWaves + wave) * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    uint64_t *tb_ = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_trace_buf)[0]; \
+    if (lane == 0 && tb_)                                                                               \
+      tb_[((size_t)blockIdx.x * kStreamWaves + wave) * 4 + (slot)] = __builtin_amdgcn_s_memrealtime();  \
   } while (0)
 #else
 #define LK_TRACE(slot) do {} while (0)
@@ -571,7 +573,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         }
       }
       if (si == 0 && row == 0) LK_TRACE(2);
+#ifdef LK_NO_REDUCE  // lab: the per-row reduction removed (wrong results)
+      const float tot = acc;
+#else
       const float tot = dpp_sum(acc);
+#endif
       if (lane == 63) out[(int64_t)row * dst_stride] = tot;
     }
   }

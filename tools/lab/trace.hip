@@ -140,6 +140,30 @@ int main(int argc, char **argv) {
   printf("\nexit by octile:");
   for (int i = 0; i < 8; i++) printf(" %6.2f", no[i] ? oct[i] / no[i] : 0);
   printf("\n");
+  // where the spread lives: inside a workgroup (its waves) or between workgroups (CUs)
+  std::vector<double> wg_max, wg_min, wg_span, wave_mean;
+  double tot = 0;
+  int cnt = 0;
+  for (int g = 0; g < grid; g++) {
+    double mx = 0, mn = 1e30;
+    for (int w = 0; w < kStreamWaves; w++) {
+      uint64_t t = h[((size_t)g * kStreamWaves + w) * 4 + 3];
+      if (!t) continue;
+      const double v = (t - t0min) * 0.01;
+      mx = std::max(mx, v); mn = std::min(mn, v);
+      tot += v; cnt++;
+    }
+    if (mx > 0) { wg_max.push_back(mx); wg_min.push_back(mn); wg_span.push_back(mx - mn); }
+  }
+  auto stats = [](const char *name, std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    auto pc = [&](double q) { return v[std::min(v.size() - 1, (size_t)(q * v.size()))]; };
+    printf("%-22s min %6.2f  p10 %6.2f  p50 %6.2f  p90 %6.2f  max %6.2f us\n", name, v.front(), pc(0.1), pc(0.5), pc(0.9), v.back());
+  };
+  stats("workgroup last exit", wg_max);
+  stats("workgroup first exit", wg_min);
+  stats("span inside workgroup", wg_span);
+  printf("mean wave exit %.2f us (a perfectly balanced launch ends about here)\n", cnt ? tot / cnt : 0.0);
 #endif
   return 0;
 }
