@@ -270,6 +270,15 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 #endif
 // Prologue order: 0 = activations then D weight units; 1 = weight unit 0, activations, units 1..D-1;
 // 2 = activations, wait for them, then the D weight units.
+#ifndef LK_STREAM_BIAS
+#define LK_STREAM_BIAS 500  // per mille of a workgroup's rows taken by waves 0..3
+#endif
+#ifndef LK_STREAM_D
+#define LK_STREAM_D 3  // weight units in flight per wave (capped by LDS)
+#endif
+#ifndef LK_TIGHT_SLOTS
+#define LK_TIGHT_SLOTS 0
+#endif
 #ifndef LK_PROLOGUE_ORDER
 #define LK_PROLOGUE_ORDER 0
 #endif
@@ -296,10 +305,12 @@ template <int QT, int CPL> struct StreamGeom {
   static constexpr int PDW = PB / 4;
   static constexpr int UB = 64 * PB;                      // bytes per unit
   static constexpr int L = (UB + 1023) / 1024;            // DMA instructions per unit
-  static constexpr int SLOT = L * 1024;
+  // LK_TIGHT_SLOTS: a slot is the unit's own bytes (the last DMA instruction's lanes past the
+  // unit are masked off) instead of L KB, so more units fit in flight
+  static constexpr int SLOT = LK_TIGHT_SLOTS ? (UB + 15) / 16 * 16 : L * 1024;
   static constexpr int IMG = 64 * CPL * 256;              // activation image: 256 B per pair
   static constexpr int DFIT = (kLdsBytes - IMG) / (kStreamWaves * SLOT);
-  static constexpr int D = DFIT < 3 ? DFIT : 3;            // ring depth (units)
+  static constexpr int D = DFIT < LK_STREAM_D ? DFIT : LK_STREAM_D;  // ring depth (units)
   static constexpr int LDS = IMG + kStreamWaves * D * SLOT;
   static constexpr int VMCNT = (D - 1) * L;               // DMA ops allowed in flight past the unit in use
   static_assert(D >= 2, "ring must double-buffer");
@@ -449,9 +460,18 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       rb = min((int)blockIdx.x * per, single.M);
       re = min(rb + per, single.M);
     }
+#if LK_STREAM_BIAS == 500
     const int per_w = (re - rb + kStreamWaves - 1) / kStreamWaves;
     const int r0 = __builtin_amdgcn_readfirstlane(min(rb + wave * per_w, re));
     const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + per_w, re) - r0);
+#else
+    // waves 0..3 take LK_STREAM_BIAS/1000 of the rows (lab: uneven split between SIMD partners)
+    const int R = re - rb, Ra = (int)((int64_t)R * LK_STREAM_BIAS / 1000);
+    const int pa = (Ra + 3) / 4, pb = (R - min(4 * pa, R) + 3) / 4;
+    const int beg = wave < 4 ? rb + wave * pa : min(rb + 4 * pa, re) + (wave - 4) * pb;
+    const int r0 = __builtin_amdgcn_readfirstlane(min(beg, re));
+    const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + (wave < 4 ? pa : pb), re) - r0);
+#endif
     const int NP = K >> 6;                         // block pairs per row
     const int nch = (NP + 63) >> 6;                // units per row
     const int64_t RB = (int64_t)NP * G::PB;        // row bytes
@@ -473,6 +493,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 #pragma unroll
       for (int j = 0; j < G::L; j++) {
         int off = j * 1024 + lane * 16;
+        if (LK_TIGHT_SLOTS) {  // lanes past the unit stay idle (their LDS bytes belong to the next slot)
+          if (off < ubytes)
+            __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + off), (LK_LDS void *)(slot + j * 1024), 16, 0,
+                                             LK_WEIGHT_AUX);
+          continue;
+        }
         off = off < ubytes ? off : 0;  // lanes past the unit re-read its first 16 B (never decoded)
         __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + off), (LK_LDS void *)(slot + j * 1024), 16, 0,
                                          LK_WEIGHT_AUX);
@@ -562,7 +588,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
           uint32_t w[G::PDW];
 #pragma unroll
           for (int k = 0; k < G::PDW; k++) w[k] = rp[k];
+#ifdef LK_NO_DECODE  // lab: the decode removed (wrong results): the DMA + LDS-read skeleton alone
+          const float v = __builtin_bit_cast(float, w[0] ^ w[G::PDW - 1]);
+#else
           const float v = pair_dot_s<QT>(w, xr[c], xs0[c], xs1[c]);
+#endif
           acc += valid[c] ? v : 0.f;
           if (issued < nunits) {
             wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it

@@ -164,6 +164,38 @@ int main(int argc, char **argv) {
   stats("workgroup first exit", wg_min);
   stats("span inside workgroup", wg_span);
   printf("mean wave exit %.2f us (a perfectly balanced launch ends about here)\n", cnt ? tot / cnt : 0.0);
+  {  // the latest workgroups: index, last exit, its waves' first-unit and exit times
+    std::vector<std::pair<double, int>> late;
+    for (int g = 0; g < grid; g++) {
+      double mx = 0;
+      for (int w = 0; w < kStreamWaves; w++) {
+        uint64_t t = h[((size_t)g * kStreamWaves + w) * 4 + 3];
+        if (t) mx = std::max(mx, (t - t0min) * 0.01);
+      }
+      late.push_back({mx, g});
+    }
+    std::sort(late.rbegin(), late.rend());
+    for (int i = 0; i < 10 && i < (int)late.size(); i++) {
+      const int g = late[i].second;
+      printf("late wg %3d (xcd %d) last exit %6.2f | 1st unit/exit per wave:", g, g % 8, late[i].first);
+      for (int w = 0; w < kStreamWaves; w++) {
+        const uint64_t *q = &h[((size_t)g * kStreamWaves + w) * 4];
+        printf(" %.1f/%.1f", q[2] ? (q[2] - t0min) * 0.01 : -1.0, q[3] ? (q[3] - t0min) * 0.01 : -1.0);
+      }
+      printf("\n");
+    }
+  }
+  // by wave index inside the workgroup: VALU arbitration favours the older wave of a SIMD pair
+  printf("mean exit by wave index:");
+  for (int w = 0; w < kStreamWaves; w++) {
+    double sw = 0; int nw = 0;
+    for (int g = 0; g < grid; g++) {
+      uint64_t t = h[((size_t)g * kStreamWaves + w) * 4 + 3];
+      if (t) { sw += (t - t0min) * 0.01; nw++; }
+    }
+    printf(" %6.2f", nw ? sw / nw : 0.0);
+  }
+  printf("\n");
 #endif
   return 0;
 }
