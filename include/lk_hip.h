@@ -31,6 +31,10 @@
  *                         (core/GGMLBackend.kt:63-69) for host-authoritative ByteArrays.
  *   lk_dequantize_device  core/GGMLComputeOps.kt:918 dequantizeTensor (Q8_0/Q4_0/Q4_1).
  *   lk_quantize_device    core/GGMLComputeOps.kt:1040 quantizeTensor (Q8_0/Q4_0/Q4_1).
+ *   lk_dot_direct*        core/GGMLComputeOps.kt:349-629 the direct dot products
+ *                         computeDotProduct{F32Q41, F32Q80, Q80Q80, Q40Q40, Q41Q41, Q80Q40}
+ *                         (graphAllocator, tensorA, tensorB, row, col, commonDimK): Float,
+ *                         evaluated for every (row, col) of A's rows x B's columns.
  *
  * Status codes map back to the exceptions the Kotlin operator throws
  * (see INTEGRATION.md for the cinterop mapping):
@@ -214,6 +218,32 @@ int lk_dequantize_device(const lk_tensor *src, float *out, void *stream);
  * reference (round-half-even, Kotlin floatToHalf). */
 int lk_quantize_device(const float *src, int64_t n_elements, int32_t type, void *out,
                        void *stream);
+
+/* ---- direct dot products (core/GGMLComputeOps.kt:349-629) -------------------
+ * Not reachable from computeMatMul in the reference; offloaded as one
+ * matrix of dots: out[row·N + col] = computeDotProduct<kind>(ga, a, b, row, col, K) for
+ * row < M = a.ne[1], col < N = b.ne[0]. A is M x K (ne[0] = K): its Q elements are read at
+ * the flat index row·K + k, its F32 elements through nb (getFloat(k, row)). B is K x N
+ * (ne[0] = N, ne[1] = K), read at the flat index k·N + col. Every element, product and sum
+ * is the Kotlin expression in the Kotlin order (sequential k, no fused multiply-add), so
+ * results are bit-identical to the reference arithmetic. */
+enum lk_dot_kind {
+  LK_DOT_F32_Q4_1 = 1, /* :349-377 computeDotProductF32Q41: f · (d·q + m)               */
+  LK_DOT_F32_Q8_0 = 2, /* :442-468 computeDotProductF32Q80: f · (d·q)                   */
+  LK_DOT_Q8_0_Q8_0 = 3, /* :474-507 computeDotProductQ80Q80: (dA·dB) · (qA·qB)           */
+  LK_DOT_Q4_0_Q4_0 = 4, /* :512-548 computeDotProductQ40Q40: dA·(nA−8) · dB·(nB−8)      */
+  LK_DOT_Q4_1_Q4_1 = 5, /* :552-589 computeDotProductQ41Q41: (dA·nA + mA)·(dB·nB + mB)  */
+  LK_DOT_Q8_0_Q4_0 = 6  /* :594-629 computeDotProductQ80Q40: dA·qA · dB·(nB−8)          */
+};
+/* Host buffers (a->data / b->data are the ByteArrays), synchronous; out: M·N floats (host).
+ * The require() checks of the Kotlin functions come first (types, a.ne[0] == K,
+ * b.ne[1] == K: LK_ERR_INVALID_ARG), then the accessors' (block index past numBlocks:
+ * LK_ERR_INVALID_ARG; bytes past the buffer: LK_ERR_OUT_OF_BOUNDS; no buffer:
+ * LK_ERR_NO_BUFFER). Unknown kind: LK_ERR_NOT_IMPLEMENTED. */
+int lk_dot_direct(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t K, float *out);
+/* The same over device buffers, enqueued on `stream` (NULL: the library's stream). */
+int lk_dot_direct_device(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t K, float *out,
+                         void *stream);
 
 #ifdef __cplusplus
 }

@@ -1465,3 +1465,113 @@ uint64_t lk_graph_transfer_bytes(const lk_graph *g, int to_device) {
 }
 
 }  // extern "C"
+
+// ---- direct dot products (core/GGMLComputeOps.kt:349-629) --------------------------------
+
+namespace {
+
+struct DotCheck {
+  int64_t M, N;
+  uint64_t a_lo, a_hi, b_lo, b_hi;  // byte extents read (buffer-relative)
+};
+
+// The Kotlin functions' require()s in order, then the accessors' checks: block index past
+// numBlocks (IllegalArgumentException), missing buffer, bytes past the buffer.
+int dot_check(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t K, DotCheck *c) {
+  int32_t ta, tb;
+  switch (kind) {
+    case LK_DOT_F32_Q4_1: ta = LK_TYPE_F32; tb = LK_TYPE_Q4_1; break;
+    case LK_DOT_F32_Q8_0: ta = LK_TYPE_F32; tb = LK_TYPE_Q8_0; break;
+    case LK_DOT_Q8_0_Q8_0: ta = LK_TYPE_Q8_0; tb = LK_TYPE_Q8_0; break;
+    case LK_DOT_Q4_0_Q4_0: ta = LK_TYPE_Q4_0; tb = LK_TYPE_Q4_0; break;
+    case LK_DOT_Q4_1_Q4_1: ta = LK_TYPE_Q4_1; tb = LK_TYPE_Q4_1; break;
+    case LK_DOT_Q8_0_Q4_0: ta = LK_TYPE_Q8_0; tb = LK_TYPE_Q4_0; break;
+    default: return fail(LK_ERR_NOT_IMPLEMENTED, "direct dot kind %d", kind);
+  }
+  if (!a || !b) return fail(LK_ERR_INVALID_ARG, "null tensor");
+  if (a->type != ta) return fail(LK_ERR_INVALID_ARG, "tensorA must be type %d. Got %d", ta, a->type);
+  if (b->type != tb) return fail(LK_ERR_INVALID_ARG, "tensorB must be type %d. Got %d", tb, b->type);
+  if (a->ne[0] != K) return fail(LK_ERR_INVALID_ARG, "tensorA K dim (%lld) must match commonDimK (%lld)", (long long)a->ne[0], (long long)K);
+  if (b->ne[1] != K) return fail(LK_ERR_INVALID_ARG, "tensorB K dim (%lld) must match commonDimK (%lld)", (long long)b->ne[1], (long long)K);
+  c->M = a->ne[1];
+  c->N = b->ne[0];
+  c->a_lo = c->a_hi = a->data_offset;
+  c->b_lo = c->b_hi = b->data_offset;
+  if (c->M <= 0 || c->N <= 0 || K <= 0) return LK_OK;  // no accessor runs
+  if (!a->data || !b->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
+  // flat indices reach M·K − 1 (A, Q types) and K·N − 1 (B)
+  auto q_extent = [](const lk_tensor *t, int64_t last_flat, uint64_t *hi) {
+    const int64_t blk = last_flat / 32, nblk = t_num_elements(t) / 32;
+    if (blk >= nblk) return fail(LK_ERR_INVALID_ARG, "blockIndex %lld out of bounds for %lld blocks", (long long)blk, (long long)nblk);
+    *hi = t->data_offset + (uint64_t)(blk + 1) * block_bytes(t->type);
+    return (int)LK_OK;
+  };
+  int rc;
+  if (ta == LK_TYPE_F32) {
+    if (a->nb[0] < 4 || a->nb[0] % 4 || a->nb[1] % 4)
+      return fail(LK_ERR_NOT_IMPLEMENTED, "direct dot: F32 strides %llu/%llu not offloaded", (unsigned long long)a->nb[0],
+                  (unsigned long long)a->nb[1]);
+    c->a_hi = a->data_offset + (uint64_t)(K - 1) * a->nb[0] + (uint64_t)(c->M - 1) * a->nb[1] + 4;
+  } else if ((rc = q_extent(a, c->M * K - 1, &c->a_hi))) {
+    return rc;
+  }
+  if ((rc = q_extent(b, K * c->N - 1, &c->b_hi))) return rc;
+  if (c->a_hi > a->buf_bytes) return fail(LK_ERR_OUT_OF_BOUNDS, "tensorA read past its buffer (%llu > %llu)", (unsigned long long)c->a_hi, (unsigned long long)a->buf_bytes);
+  if (c->b_hi > b->buf_bytes) return fail(LK_ERR_OUT_OF_BOUNDS, "tensorB read past its buffer (%llu > %llu)", (unsigned long long)c->b_hi, (unsigned long long)b->buf_bytes);
+  return LK_OK;
+}
+
+int launch_dot_direct(int32_t kind, const uint8_t *a, const uint8_t *b, const lk_tensor *at, int64_t M, int64_t N, int64_t K, float *out,
+                      hipStream_t st) {
+  if (M * N == 0) return LK_OK;
+  if (K == 0) { HIP_TRY(hipMemsetAsync(out, 0, (size_t)(M * N) * sizeof(float), st)); return LK_OK; }
+  DotArgs g{a, b, out, M, N, K, (int64_t)at->nb[0], (int64_t)at->nb[1]};
+  const int64_t blocks = (M * N + 255) / 256;
+  if (blocks > (int64_t)INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "direct dot: output too large");
+  dim3 grid((unsigned)blocks), block(256);
+  switch (kind) {
+    case LK_DOT_F32_Q4_1: hipLaunchKernelGGL(dot_direct_kernel<LK_DOT_F32_Q4_1>, grid, block, 0, st, g); break;
+    case LK_DOT_F32_Q8_0: hipLaunchKernelGGL(dot_direct_kernel<LK_DOT_F32_Q8_0>, grid, block, 0, st, g); break;
+    case LK_DOT_Q8_0_Q8_0: hipLaunchKernelGGL(dot_direct_kernel<LK_DOT_Q8_0_Q8_0>, grid, block, 0, st, g); break;
+    case LK_DOT_Q4_0_Q4_0: hipLaunchKernelGGL(dot_direct_kernel<LK_DOT_Q4_0_Q4_0>, grid, block, 0, st, g); break;
+    case LK_DOT_Q4_1_Q4_1: hipLaunchKernelGGL(dot_direct_kernel<LK_DOT_Q4_1_Q4_1>, grid, block, 0, st, g); break;
+    default: hipLaunchKernelGGL(dot_direct_kernel<LK_DOT_Q8_0_Q4_0>, grid, block, 0, st, g); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+}  // namespace
+
+int lk_dot_direct_device(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t K, float *out, void *stream) {
+  DotCheck c;
+  int rc = dot_check(kind, a, b, K, &c);
+  if (rc) return rc;
+  if (c.M <= 0 || c.N <= 0) return LK_OK;
+  if (!out) return fail(LK_ERR_NO_BUFFER, "output buffer not found");
+  if ((rc = ensure_init())) return rc;
+  return launch_dot_direct(kind, (const uint8_t *)a->data + a->data_offset, (const uint8_t *)b->data + b->data_offset, a, c.M, c.N, K,
+                           out, pick_stream(stream));
+}
+
+int lk_dot_direct(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t K, float *out) {
+  DotCheck c;
+  int rc = dot_check(kind, a, b, K, &c);
+  if (rc) return rc;
+  if (c.M <= 0 || c.N <= 0) return LK_OK;
+  if (!out) return fail(LK_ERR_NO_BUFFER, "output buffer not found");
+  if ((rc = ensure_init())) return rc;
+  Dev &s = cur();
+  hipStream_t st = s.stream;
+  const uint64_t a_bytes = c.a_hi - c.a_lo, b_bytes = c.b_hi - c.b_lo, o_bytes = (uint64_t)(c.M * c.N) * sizeof(float);
+  if ((rc = ensure_scratch(s, 0, std::max<uint64_t>(a_bytes, 16)))) return rc;
+  if ((rc = ensure_scratch(s, 1, std::max<uint64_t>(b_bytes, 16)))) return rc;
+  if ((rc = ensure_scratch(s, 2, o_bytes))) return rc;
+  if (a_bytes) HIP_TRY(hipMemcpyAsync(s.scratch[0], (const uint8_t *)a->data + c.a_lo, a_bytes, hipMemcpyHostToDevice, st));
+  if (b_bytes) HIP_TRY(hipMemcpyAsync(s.scratch[1], (const uint8_t *)b->data + c.b_lo, b_bytes, hipMemcpyHostToDevice, st));
+  rc = launch_dot_direct(kind, (const uint8_t *)s.scratch[0], (const uint8_t *)s.scratch[1], a, c.M, c.N, K, (float *)s.scratch[2], st);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out, s.scratch[2], o_bytes, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return LK_OK;
+}

@@ -2042,4 +2042,71 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float *__restrict__
   }
 }
 
+// ---- direct dot products (computeDotProduct{F32Q41, F32Q80, Q80Q80, Q40Q40, Q41Q41, Q80Q40},
+// GGMLComputeOps.kt:349-629) ----------------------------------------------------------------
+// One thread per (row, col), k in order, every element / product / sum the Kotlin expression
+// with explicit roundings: bit-identical to the reference arithmetic. Dead code in the
+// reference (not reachable from computeMatMul): correctness, not speed, is the point; lanes
+// of a wave share the row (A reads broadcast) and take consecutive columns (B reads coalesce).
+struct DotArgs {
+  const uint8_t *a, *b;  // buffer base + dataOffset
+  float *out;            // [M][N]
+  int64_t M, N, K;
+  int64_t a_nb0, a_nb1;  // F32 A (getFloat(k, row) honours nb)
+};
+
+// Q element at a flat index: Q8_0 d·q, Q4_0 d·(n − 8), Q4_1 d·n + m (accessor order). Plain
+// operators under contract(off): __fmul_rn / __fadd_rn carry the header's own contraction
+// flags and were seen fused into an FMA once inlined next to an add.
+template <int QT> __device__ __forceinline__ float q_elem(const uint8_t *base, int64_t flat) {
+#pragma clang fp contract(off)
+  const uint8_t *p = base + (flat >> 5) * QTraits<QT>::BB;
+  const int item = (int)(flat & 31);
+  const float d = h2f(ld_u16(p));
+  if constexpr (QT == LK_TYPE_Q8_0) {
+    return d * (float)(int32_t)(int8_t)ld_u8(p + 2 + item);
+  } else if constexpr (QT == LK_TYPE_Q4_1) {
+    const float m = h2f(ld_u16(p + 2));
+    const uint32_t byte = ld_u8(p + 4 + (item >> 1));
+    const float dq = d * (float)((item & 1) ? (byte >> 4) : (byte & 0xF));
+    return dq + m;
+  } else {
+    const uint32_t byte = ld_u8(p + 2 + (item >> 1));
+    const float qm = (float)((item & 1) ? (byte >> 4) : (byte & 0xF)) - 8.0f;
+    return d * qm;
+  }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void dot_direct_kernel(DotArgs g) {
+#pragma clang fp contract(off)
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= g.M * g.N) return;
+  const int64_t i = idx / g.N, j = idx % g.N;
+  float sum = 0.f;
+  for (int64_t k = 0; k < g.K; k++) {
+    const int64_t fb = k * g.N + j;
+    float p;
+    if constexpr (KIND == LK_DOT_F32_Q4_1 || KIND == LK_DOT_F32_Q8_0) {
+      const float f = *(const float *)(g.a + k * g.a_nb0 + i * g.a_nb1);
+      const float w = q_elem<KIND == LK_DOT_F32_Q4_1 ? LK_TYPE_Q4_1 : LK_TYPE_Q8_0>(g.b, fb);
+      p = f * w;
+    } else if constexpr (KIND == LK_DOT_Q8_0_Q8_0) {  // (dA·dB)·(qA·qB)
+      const int64_t fa = i * g.K + k;
+      const uint8_t *pa = g.a + (fa >> 5) * 34, *pb = g.b + (fb >> 5) * 34;
+      const float s2 = h2f(ld_u16(pa)) * h2f(ld_u16(pb));
+      const float q2 = (float)(int32_t)(int8_t)ld_u8(pa + 2 + (int)(fa & 31)) * (float)(int32_t)(int8_t)ld_u8(pb + 2 + (int)(fb & 31));
+      p = s2 * q2;
+    } else {
+      constexpr int TA = KIND == LK_DOT_Q4_1_Q4_1 ? LK_TYPE_Q4_1 : KIND == LK_DOT_Q8_0_Q4_0 ? LK_TYPE_Q8_0 : LK_TYPE_Q4_0;
+      constexpr int TB = KIND == LK_DOT_Q4_1_Q4_1 ? LK_TYPE_Q4_1 : LK_TYPE_Q4_0;
+      const float wa = q_elem<TA>(g.a, i * g.K + k);
+      const float wb = q_elem<TB>(g.b, fb);
+      p = wa * wb;
+    }
+    sum = sum + p;
+  }
+  g.out[idx] = sum;
+}
+
 }  // namespace lk

@@ -7,6 +7,7 @@ C-ABI in include/lk_hip.h (liblk_hip.so, hand-written HIP kernels):
   GGMLTensor / GGMLGraphAllocator / GGMLType          core/GGMLTypes.kt, core/GGMLAlloc.kt
   GGMLHipBackend (GGMLBackend)                        core/GGMLBackend.kt:90-157
   dequantizeTensor / quantizeTensor (device)          core/GGMLComputeOps.kt:918 / :1040
+  computeDotProductMatrix (direct Q x Q / F32 x Q)    core/GGMLComputeOps.kt:349-629
   RowShardedMulMat (rows over GPUs + RCCL gather)     new: the reference is single-device
   GGUFParser / ModelLoader / LoadedModel              gguf/GGUFParser.kt, gguf/ModelLoader.kt
 
@@ -16,8 +17,10 @@ from . import _lib
 from ._lib import (HipDeviceError, IllegalArgumentException, IllegalStateException, IndexOutOfBoundsException,
                    NotOffloadedError)
 from .backend import GGMLBackendRegistry, GGMLHipBackend, GGMLStatus
-from .ops import (MulMatPlan, ResidentGraph, computeMatMul, computeMatMulSharded, dequantizeTensor, quantizeTensor, to_lk, validateMatMul, weightsEvictAll,
-                  weightsPin, weightsPinSharded)
+from .ops import (DotKind, MulMatPlan, ResidentGraph, computeDotProductF32Q41, computeDotProductF32Q80, computeDotProductMatrix,
+                  computeDotProductQ40Q40, computeDotProductQ41Q41, computeDotProductQ80Q40, computeDotProductQ80Q80, computeMatMul,
+                  computeMatMulSharded, dequantizeTensor, quantizeTensor, to_lk, validateMatMul, weightsEvictAll, weightsPin,
+                  weightsPinSharded)
 from .gguf import GGUFContext, GGUFParser, GGUFTensorInfo, GGUFType, LoadedModel, ModelLoader
 from .sharded import RowShardedMulMat, row_slice, shard_rows
 from .tensor import (GGMLCGraph, GGMLContext, GGMLGraphAllocator, GGMLOp, GGMLTensor, GGMLType,
@@ -27,7 +30,9 @@ __all__ = [
     "GGMLType", "GGMLTensor", "GGMLGraphAllocator", "GGMLContext", "GGMLCGraph", "GGMLOp",
     "calculateContiguousStrides", "calculateTensorByteSize",
     "computeMatMul", "computeMatMulSharded", "weightsPinSharded", "validateMatMul", "MulMatPlan", "ResidentGraph", "dequantizeTensor", "quantizeTensor", "weightsPin",
-    "weightsEvictAll", "to_lk",
+    "weightsEvictAll", "to_lk", "DotKind", "computeDotProductMatrix", "computeDotProductF32Q41",
+    "computeDotProductF32Q80", "computeDotProductQ80Q80", "computeDotProductQ40Q40", "computeDotProductQ41Q41",
+    "computeDotProductQ80Q40",
     "GGMLHipBackend", "GGMLStatus", "GGMLBackendRegistry",
     "RowShardedMulMat", "row_slice", "shard_rows",
     "GGUFParser", "GGUFContext", "GGUFTensorInfo", "GGUFType", "ModelLoader", "LoadedModel",

@@ -78,7 +78,7 @@ EXPORTED_SYMBOLS = (
     "lk_graph_create", "lk_graph_compute", "lk_graph_num_levels", "lk_graph_num_launches",
     "lk_graph_transfer_bytes", "lk_graph_destroy",
     "lk_weights_pin", "lk_weights_evict_all", "lk_weights_cached_bytes",
-    "lk_dequantize_device", "lk_quantize_device",
+    "lk_dequantize_device", "lk_quantize_device", "lk_dot_direct", "lk_dot_direct_device",
     # include/lk_gguf.h
     "lk_gguf_open_memory", "lk_gguf_open_file", "lk_gguf_close", "lk_gguf_version", "lk_gguf_alignment",
     "lk_gguf_data_offset", "lk_gguf_data_bytes", "lk_gguf_kv_count", "lk_gguf_find_key", "lk_gguf_kv_key",
@@ -134,6 +134,8 @@ def load():
     L.lk_weights_cached_bytes.restype = ctypes.c_uint64
     L.lk_dequantize_device.argtypes = [P, vp, vp]
     L.lk_quantize_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp]
+    L.lk_dot_direct.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, vp]
+    L.lk_dot_direct_device.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, vp, vp]
     # GGUF (include/lk_gguf.h); handles are opaque void*
     u64, i64, i32, pvp, pu64 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)
     L.lk_gguf_open_memory.argtypes = [vp, u64, i32, pvp]

@@ -9,6 +9,10 @@
   dequantizeTensor / quantizeTensor
       core/GGMLComputeOps.kt:918 / :1040, on device (the format steps either side of the
       path).
+  computeDotProductMatrix(kind, graphAllocator, a, b, K) and computeDotProduct{F32Q41, F32Q80,
+      Q80Q80, Q40Q40, Q41Q41, Q80Q40}
+      core/GGMLComputeOps.kt:349-629, the direct dot products (not reachable from
+      computeMatMul in the reference), every (row, col) in one launch.
 
 Device buffers go through lk_mul_mat_device on the current torch stream (asynchronous,
 no host sync); host buffers through lk_mul_mat (the Kotlin ByteArray drop-in).
@@ -228,6 +232,56 @@ def quantizeTensor(src, targetType: GGMLType, stream=None):
         _lib.check(L.lk_quantize_device(ctypes.c_void_p(src.data_ptr()), n, int(targetType),
                                         ctypes.c_void_p(out.data_ptr() if out.numel() else 0), sh))
     return out
+
+
+class DotKind:
+    """lk_dot_kind (include/lk_hip.h): the direct dot products of core/GGMLComputeOps.kt:349-629."""
+    F32_Q4_1 = 1   # computeDotProductF32Q41 :349
+    F32_Q8_0 = 2   # computeDotProductF32Q80 :442
+    Q8_0_Q8_0 = 3  # computeDotProductQ80Q80 :474
+    Q4_0_Q4_0 = 4  # computeDotProductQ40Q40 :512
+    Q4_1_Q4_1 = 5  # computeDotProductQ41Q41 :552
+    Q8_0_Q4_0 = 6  # computeDotProductQ80Q40 :594
+
+
+def computeDotProductMatrix(kind: int, graphAllocator: GGMLGraphAllocator, tensorA: GGMLTensor, tensorB: GGMLTensor,
+                            commonDimK: int, stream=None):
+    """Every computeDotProduct<kind>(graphAllocator, tensorA, tensorB, row, col, commonDimK) for
+    row < tensorA.ne[1], col < tensorB.ne[0], as an [M, N] float32 array (numpy for host buffers,
+    a torch tensor on the buffers' device otherwise). Bit-identical to the Kotlin arithmetic."""
+    L = _lib.load()
+    la, lb = to_lk(graphAllocator, tensorA), to_lk(graphAllocator, tensorB)
+    M, N = max(int(tensorA.ne[1]), 0), max(int(tensorB.ne[0]), 0)
+    host = [_is_host(graphAllocator, t) for t in (tensorA, tensorB)]
+    if all(host):
+        out = np.zeros((M, N), dtype=np.float32)
+        _lib.check(L.lk_dot_direct(int(kind), ctypes.byref(la), ctypes.byref(lb), int(commonDimK),
+                                   ctypes.c_void_p(out.ctypes.data if out.size else 0)))
+        return out
+    if any(host):
+        raise _lib.IllegalArgumentException("operands must all be host or all be device buffers")
+    import torch
+    out = torch.zeros((M, N), dtype=torch.float32, device=graphAllocator.buffers[tensorA.bufferId].device)
+    with _OnStream(stream) as sh:
+        _lib.check(L.lk_dot_direct_device(int(kind), ctypes.byref(la), ctypes.byref(lb), int(commonDimK),
+                                          ctypes.c_void_p(out.data_ptr() if out.numel() else 0), sh))
+    return out
+
+
+def _dot_one(kind):
+    def f(graphAllocator: GGMLGraphAllocator, tensorA: GGMLTensor, tensorB: GGMLTensor, rowIndex: int, colIndex: int,
+          commonDimK: int) -> float:
+        return float(computeDotProductMatrix(kind, graphAllocator, tensorA, tensorB, commonDimK)[rowIndex, colIndex])
+    return f
+
+
+# the reference's per-(row, col) functions, by name (each evaluates the whole matrix: a test convenience)
+computeDotProductF32Q41 = _dot_one(DotKind.F32_Q4_1)
+computeDotProductF32Q80 = _dot_one(DotKind.F32_Q8_0)
+computeDotProductQ80Q80 = _dot_one(DotKind.Q8_0_Q8_0)
+computeDotProductQ40Q40 = _dot_one(DotKind.Q4_0_Q4_0)
+computeDotProductQ41Q41 = _dot_one(DotKind.Q4_1_Q4_1)
+computeDotProductQ80Q40 = _dot_one(DotKind.Q8_0_Q4_0)
 
 
 def weightsPin(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, generation: int = 0):

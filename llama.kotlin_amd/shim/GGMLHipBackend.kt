@@ -85,6 +85,39 @@ fun computeMatMulHip(graphAllocator: GGMLGraphAllocator, @Suppress("unused") con
     }
 }
 
+/**
+ * The direct dot products computeDotProduct{F32Q41, F32Q80, Q80Q80, Q40Q40, Q41Q41, Q80Q40}
+ * (core/GGMLComputeOps.kt:349-629) for every (row, col) of tensorA's rows x tensorB's columns
+ * in one call: out[row * N + col], bit-identical to the Kotlin functions (same element
+ * expressions, k in order, no fused multiply-add). kind = LK_DOT_* of lk_hip.h.
+ */
+fun computeDotProductMatrixHip(graphAllocator: GGMLGraphAllocator, kind: Int, tensorA: GGMLTensor,
+                               tensorB: GGMLTensor, commonDimK: Int): FloatArray {
+    val bufA = graphAllocator.buffers.getOrNull(tensorA.bufferId)
+    val bufB = graphAllocator.buffers.getOrNull(tensorB.bufferId)
+    val out = FloatArray(maxOf(tensorA.ne[1].toInt(), 0) * maxOf(tensorB.ne[0].toInt(), 0))
+    memScoped {
+        val la = alloc<lk_tensor>()
+        val lb = alloc<lk_tensor>()
+        (bufA ?: ByteArray(0)).usePinned { pa ->
+            (bufB ?: ByteArray(0)).usePinned { pb ->
+                out.usePinned { po ->
+                    fill(la, tensorA, if (bufA != null && bufA.isNotEmpty()) pa.addressOf(0) else null, bufA?.size ?: 0)
+                    fill(lb, tensorB, if (bufB != null && bufB.isNotEmpty()) pb.addressOf(0) else null, bufB?.size ?: 0)
+                    checkStatus(lk_dot_direct(kind, la.ptr, lb.ptr, commonDimK.toLong(),
+                                              if (out.isNotEmpty()) po.addressOf(0) else null))
+                }
+            }
+        }
+    }
+    return out
+}
+
+/** computeDotProductQ80Q80(graphAllocator, a, b, row, col, K) through the matrix call (one element). */
+fun computeDotProductQ80Q80Hip(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, b: GGMLTensor,
+                               row: Int, col: Int, commonDimK: Int): Float =
+    computeDotProductMatrixHip(graphAllocator, LK_DOT_Q8_0_Q8_0, a, b, commonDimK)[row * b.ne[0].toInt() + col]
+
 /** A GGMLBackend that offloads MUL_MAT to the MI355X and defers everything else to the CPU backend. */
 class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) : GGMLBackend {
     private val cpu = GGMLCpuBackend()

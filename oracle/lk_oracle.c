@@ -842,3 +842,101 @@ int lko_compute_mat_mul_tight(const lk_tensor *a, const lk_tensor *b, lk_tensor 
   }
   return LK_OK;
 }
+
+/* ---- direct dot products (core/GGMLComputeOps.kt:349-629) --------------------------------
+ * Unreachable from computeMatMul in the reference; restated for the lk_dot_direct offload.
+ * A: M x K (ne[0] = K), Q elements at the flat index row*K + k, F32 through getFloat(k, row).
+ * B: K x N (ne[0] = N, ne[1] = K), flat index k*N + col. Each function first runs its
+ * require()s (types, A.ne[0] == K, B.ne[1] == K), then the accessors in the Kotlin order. */
+
+/* one Q element of t at flat index `flat`: Q8_0 -> d*q; Q4_0 -> d*(n - 8); Q4_1 -> d*n + m
+ * (the expressions of :366-367, :461-462, :498-505, :539-541, :579-581, :620-621) */
+static float q_elem(const lk_tensor *t, int64_t flat, int *st) {
+  int64_t blk = flat / 32;
+  int32_t item = (int32_t)(flat % 32);
+  float d = q_scale(t, t->type, blk, st); if (*st) return 0;
+  if (t->type == LK_TYPE_Q8_0) {
+    int32_t q = q8_weight(t, blk, item, st); if (*st) return 0;
+    return d * (float)q;
+  }
+  if (t->type == LK_TYPE_Q4_1) {
+    float m = q41_min(t, blk, st); if (*st) return 0;
+    int32_t q = q4_nibble(t, LK_TYPE_Q4_1, blk, item, st); if (*st) return 0;
+    float dq = d * (float)q;
+    return dq + m;
+  }
+  int32_t q = q4_nibble(t, LK_TYPE_Q4_0, blk, item, st); if (*st) return 0;
+  float qm = (float)q - 8.0f;
+  return d * qm;
+}
+
+static int dot_kind_types(int32_t kind, int32_t *ta, int32_t *tb) {
+  switch (kind) {
+    case LK_DOT_F32_Q4_1: *ta = LK_TYPE_F32; *tb = LK_TYPE_Q4_1; return 1;
+    case LK_DOT_F32_Q8_0: *ta = LK_TYPE_F32; *tb = LK_TYPE_Q8_0; return 1;
+    case LK_DOT_Q8_0_Q8_0: *ta = LK_TYPE_Q8_0; *tb = LK_TYPE_Q8_0; return 1;
+    case LK_DOT_Q4_0_Q4_0: *ta = LK_TYPE_Q4_0; *tb = LK_TYPE_Q4_0; return 1;
+    case LK_DOT_Q4_1_Q4_1: *ta = LK_TYPE_Q4_1; *tb = LK_TYPE_Q4_1; return 1;
+    case LK_DOT_Q8_0_Q4_0: *ta = LK_TYPE_Q8_0; *tb = LK_TYPE_Q4_0; return 1;
+    default: return 0;
+  }
+}
+
+int lko_dot_direct(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t row, int64_t col, int64_t K, float *out) {
+  int32_t ta, tb;
+  if (!dot_kind_types(kind, &ta, &tb)) return fail(LK_ERR_NOT_IMPLEMENTED, "direct dot kind %d", kind);
+  if (a->type != ta) return fail(LK_ERR_INVALID_ARG, "tensorA must be type %d. Got %d", ta, a->type);
+  if (b->type != tb) return fail(LK_ERR_INVALID_ARG, "tensorB must be type %d. Got %d", tb, b->type);
+  if (a->ne[0] != K) return fail(LK_ERR_INVALID_ARG, "tensorA K dim (%lld) must match commonDimK (%lld)", (long long)a->ne[0], (long long)K);
+  if (b->ne[1] != K) return fail(LK_ERR_INVALID_ARG, "tensorB K dim (%lld) must match commonDimK (%lld)", (long long)b->ne[1], (long long)K);
+  const int64_t N = b->ne[0];
+  int st = LK_OK;
+  float sum = 0.0f;
+  for (int64_t k = 0; k < K; k++) {
+    const int64_t flat_b = k * N + col;
+    float p;
+    switch (kind) {
+      case LK_DOT_F32_Q4_1:   /* :364-375 */
+      case LK_DOT_F32_Q8_0: { /* :457-466 */
+        float f = get_float(a, k, row, &st); if (st) return st;
+        float w = q_elem(b, flat_b, &st); if (st) return st;
+        p = f * w;
+        break;
+      }
+      case LK_DOT_Q8_0_Q8_0: { /* :488-505: scaleA * scaleB * (qA * qB) */
+        int64_t fa = row * K + k;
+        float sa = q_scale(a, LK_TYPE_Q8_0, fa / 32, &st); if (st) return st;
+        int32_t qa = q8_weight(a, fa / 32, (int32_t)(fa % 32), &st); if (st) return st;
+        float sb = q_scale(b, LK_TYPE_Q8_0, flat_b / 32, &st); if (st) return st;
+        int32_t qb = q8_weight(b, flat_b / 32, (int32_t)(flat_b % 32), &st); if (st) return st;
+        float s2 = sa * sb;
+        float q2 = (float)qa * (float)qb;
+        p = s2 * q2;
+        break;
+      }
+      default: { /* Q40Q40 :526-546, Q41Q41 :566-587, Q80Q40 :608-627: dequantA * dequantB */
+        float wa = q_elem(a, row * K + k, &st); if (st) return st;
+        float wb = q_elem(b, flat_b, &st); if (st) return st;
+        p = wa * wb;
+        break;
+      }
+    }
+    sum = sum + p;
+  }
+  *out = sum;
+  return LK_OK;
+}
+
+int lko_dot_direct_matrix(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t K, float *out) {
+  const int64_t M = a->ne[1], N = b->ne[0];
+  for (int64_t i = 0; i < M; i++)
+    for (int64_t j = 0; j < N; j++) {
+      int st = lko_dot_direct(kind, a, b, i, j, K, out + i * N + j);
+      if (st) return st;
+    }
+  if (M == 0 || N == 0) {  /* the requires still run once a caller would have called the function */
+    int32_t ta, tb;
+    if (!dot_kind_types(kind, &ta, &tb)) return fail(LK_ERR_NOT_IMPLEMENTED, "direct dot kind %d", kind);
+  }
+  return LK_OK;
+}

@@ -53,6 +53,12 @@ int lko_compute_mat_mul(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst);
  * CPU variant for the baseline); only Q4_0/Q4_1/Q8_0 x F32, contiguous B/dst. */
 int lko_compute_mat_mul_tight(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst);
 
+/* The direct dot products computeDotProduct{F32Q41, F32Q80, Q80Q80, Q40Q40, Q41Q41,
+ * Q80Q40} (core/GGMLComputeOps.kt:349-629), kind = lk_dot_kind: one dot, and every
+ * (row, col) of a.ne[1] x b.ne[0] into out (row-major). */
+int lko_dot_direct(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t row, int64_t col, int64_t K, float *out);
+int lko_dot_direct_matrix(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t K, float *out);
+
 /* Batch forms of the conversions (for exhaustive tests). */
 void lko_half_to_float_n(const uint16_t *in, float *out, int64_t n);
 void lko_float_to_half_n(const float *in, uint16_t *out, int64_t n);

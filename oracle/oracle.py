@@ -71,6 +71,9 @@ def lib():
         L.lko_dequantize.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
         L.lko_compute_mat_mul.argtypes = [P, P, P]
         L.lko_compute_mat_mul_tight.argtypes = [P, P, P]
+        L.lko_dot_direct.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.POINTER(ctypes.c_float)]
+        L.lko_dot_direct_matrix.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, ctypes.c_void_p]
         L.lko_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -184,3 +187,20 @@ def mat_mul_q(qtype: int, a_blocks: np.ndarray, M: int, K: int, x: np.ndarray, t
     st = (compute_mat_mul_tight if tight else compute_mat_mul)(a, b, d)
     _check(st)
     return dbuf.view(np.float32).reshape(M, N)
+
+
+def dot_direct_matrix(kind: int, a: LkTensor, b: LkTensor, K: int) -> tuple[int, np.ndarray]:
+    """lko_dot_direct_matrix: (status, [a.ne[1], b.ne[0]] float32) — the direct dot products of
+    core/GGMLComputeOps.kt:349-629 for every (row, col), Kotlin arithmetic order."""
+    M, N = max(int(a.ne[1]), 0), max(int(b.ne[0]), 0)
+    out = np.zeros((M, N), dtype=np.float32)
+    st = lib().lko_dot_direct_matrix(int(kind), ctypes.byref(a), ctypes.byref(b), int(K),
+                                     out.ctypes.data if out.size else None)
+    return st, out
+
+
+def dot_direct(kind: int, a: LkTensor, b: LkTensor, row: int, col: int, K: int) -> tuple[int, float]:
+    """lko_dot_direct: one computeDotProduct<kind>(ga, a, b, row, col, K)."""
+    v = ctypes.c_float(0.0)
+    st = lib().lko_dot_direct(int(kind), ctypes.byref(a), ctypes.byref(b), int(row), int(col), int(K), ctypes.byref(v))
+    return st, float(v.value)
