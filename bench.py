@@ -506,11 +506,31 @@ def cpu_baseline(sample_rows, token_bytes):
         total_t += time.perf_counter() - t0
         total_b += alg_bytes(rows, K)
     gbs = total_b / total_t / 1e9
-    return {"value": round(gbs, 5), "unit": "GB/s", "cores": 1, "kind": "port",
-            "tokens_per_s": round(gbs * 1e9 / token_bytes, 6),
-            "sample": f"structural C restatement of computeMatMul (oracle/lk_oracle.c), Q4_0 x F32 N=1, "
-                      f"first {sample_rows} rows of each of the 7 Llama-7B layer matrices ({total_b} algorithmic bytes, "
-                      f"{total_t:.2f} s), single thread"}
+    out = {"value": round(gbs, 5), "unit": "GB/s", "cores": 1, "kind": "port",
+           "tokens_per_s": round(gbs * 1e9 / token_bytes, 6),
+           "sample": f"structural C restatement of computeMatMul (oracle/lk_oracle.c), Q4_0 x F32 N=1, "
+                     f"first {sample_rows} rows of each of the 7 Llama-7B layer matrices ({total_b} algorithmic bytes, "
+                     f"{total_t:.2f} s), single thread"}
+    # SURVEY §8d's other two CPU lines: the same arithmetic without the accessor overhead
+    # ("tight"), on one thread and with rows split over the host's cores (OpenMP)
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    variants = {}
+    for label, nthr, rows_cap in (("tight_1_thread", 1, 4096), (f"tight_{threads}_threads", threads, None)):
+        tb, tt = 0, 0.0
+        for (name, M, K) in LAYER_MATS:
+            rows = M if rows_cap is None else min(rows_cap, M)
+            q = O.quantize(O.Q4_0, (rng.standard_normal(rows * K) * 0.02).astype(np.float32))
+            x = rng.standard_normal((K, 1)).astype(np.float32)
+            t0 = time.perf_counter()
+            O.mat_mul_q(O.Q4_0, q, rows, K, x, tight=True, threads=nthr)
+            tt += time.perf_counter() - t0
+            tb += alg_bytes(rows, K)
+        g = tb / tt / 1e9
+        variants[label] = {"value": round(g, 4), "unit": "GB/s", "cores": nthr, "tokens_per_s": round(g * 1e9 / token_bytes, 4),
+                           "sample": f"{'all rows' if rows_cap is None else f'first {rows_cap} rows'} of each layer matrix, "
+                                     f"{tb} algorithmic bytes, {tt:.2f} s"}
+    out["variants"] = variants
+    return out
 
 
 if __name__ == "__main__":

@@ -793,26 +793,17 @@ int lko_compute_mat_mul(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) 
 /* "tight" CPU baseline: identical arithmetic order to the structural path for
  * Q4_0/Q4_1/Q8_0 x F32 with contiguous B/dst and K % 32 == 0, without the
  * per-element accessor overhead. Results are bit-identical to lko_compute_mat_mul. */
-int lko_compute_mat_mul_tight(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
-  int64_t M = a->ne[1], K = a->ne[0], N = b->ne[0];
-  if (K != b->ne[1] || dst->ne[0] != N || dst->ne[1] != M) return fail(LK_ERR_INVALID_ARG, "shape mismatch");
-  if (K % 32 || b->type != LK_TYPE_F32 || dst->type != LK_TYPE_F32) return fail(LK_ERR_NOT_IMPLEMENTED, "tight path: unsupported");
-  if (b->nb[0] != 4 || b->nb[1] != 4 * (uint64_t)N || dst->nb[0] != 4 || dst->nb[1] != 4 * (uint64_t)N)
-    return fail(LK_ERR_NOT_IMPLEMENTED, "tight path: non-contiguous");
-  int bb = lko_block_bytes(a->type);
-  if (!bb) return fail(LK_ERR_NOT_IMPLEMENTED, "tight path: type");
-  const uint8_t *A = (const uint8_t *)a->data + a->data_offset;
-  const float *B = (const float *)((const uint8_t *)b->data + b->data_offset);
-  float *D = (float *)((uint8_t *)dst->data + dst->data_offset);
+/* rows [i0, i1) of the tight path: the dot expressions of :43-145 without the accessors */
+static void tight_rows(int32_t type, int bb, const uint8_t *A, const float *B, float *D, int64_t K, int64_t N, int64_t i0, int64_t i1) {
   int64_t nbk = K / 32;
-  for (int64_t i = 0; i < M; i++) {
+  for (int64_t i = i0; i < i1; i++) {
     const uint8_t *row = A + i * nbk * bb;
     for (int64_t j = 0; j < N; j++) {
       float sum = 0.0f;
       for (int64_t blk = 0; blk < nbk; blk++) {
         const uint8_t *p = row + blk * bb;
         float d = lko_half_to_float(rd_u16(p));
-        if (a->type == LK_TYPE_Q4_0) {
+        if (type == LK_TYPE_Q4_0) {
           for (int k = 0; k < 32; k++) {
             int q = (k & 1) ? (p[2 + k / 2] >> 4) : (p[2 + k / 2] & 0x0F);
             float qm = (float)q - 8.0f;
@@ -820,7 +811,7 @@ int lko_compute_mat_mul_tight(const lk_tensor *a, const lk_tensor *b, lk_tensor 
             float p2 = w * B[(blk * 32 + k) * N + j];
             sum = sum + p2;
           }
-        } else if (a->type == LK_TYPE_Q4_1) {
+        } else if (type == LK_TYPE_Q4_1) {
           float m = lko_half_to_float(rd_u16(p + 2));
           for (int k = 0; k < 32; k++) {
             int q = (k & 1) ? (p[4 + k / 2] >> 4) : (p[4 + k / 2] & 0x0F);
@@ -840,7 +831,35 @@ int lko_compute_mat_mul_tight(const lk_tensor *a, const lk_tensor *b, lk_tensor 
       D[i * N + j] = sum;
     }
   }
+}
+
+int lko_compute_mat_mul_tight_mt(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, int threads) {
+  int64_t M = a->ne[1], K = a->ne[0], N = b->ne[0];
+  if (K != b->ne[1] || dst->ne[0] != N || dst->ne[1] != M) return fail(LK_ERR_INVALID_ARG, "shape mismatch");
+  if (K % 32 || b->type != LK_TYPE_F32 || dst->type != LK_TYPE_F32) return fail(LK_ERR_NOT_IMPLEMENTED, "tight path: unsupported");
+  if (b->nb[0] != 4 || b->nb[1] != 4 * (uint64_t)N || dst->nb[0] != 4 || dst->nb[1] != 4 * (uint64_t)N)
+    return fail(LK_ERR_NOT_IMPLEMENTED, "tight path: non-contiguous");
+  int bb = lko_block_bytes(a->type);
+  if (!bb) return fail(LK_ERR_NOT_IMPLEMENTED, "tight path: type");
+  const uint8_t *A = (const uint8_t *)a->data + a->data_offset;
+  const float *B = (const float *)((const uint8_t *)b->data + b->data_offset);
+  float *D = (float *)((uint8_t *)dst->data + dst->data_offset);
+  if (threads <= 1) {
+    tight_rows(a->type, bb, A, B, D, K, N, 0, M);
+    return LK_OK;
+  }
+  /* rows are independent (each dot keeps its own k order): the parallel split is bit-identical */
+  const int64_t chunk = 16;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1)
+  for (int64_t c = 0; c < (M + chunk - 1) / chunk; c++) {
+    int64_t i0 = c * chunk, i1 = i0 + chunk < M ? i0 + chunk : M;
+    tight_rows(a->type, bb, A, B, D, K, N, i0, i1);
+  }
   return LK_OK;
+}
+
+int lko_compute_mat_mul_tight(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
+  return lko_compute_mat_mul_tight_mt(a, b, dst, 1);
 }
 
 /* ---- direct dot products (core/GGMLComputeOps.kt:349-629) --------------------------------

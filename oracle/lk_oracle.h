@@ -52,6 +52,9 @@ int lko_compute_mat_mul(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst);
 /* Same arithmetic order without the per-element accessor overhead ("tight"
  * CPU variant for the baseline); only Q4_0/Q4_1/Q8_0 x F32, contiguous B/dst. */
 int lko_compute_mat_mul_tight(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst);
+/* The tight variant with rows split over `threads` OpenMP threads (bit-identical: every
+ * dot keeps its own order). The CPU baseline's all-cores line. */
+int lko_compute_mat_mul_tight_mt(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, int threads);
 
 /* The direct dot products computeDotProduct{F32Q41, F32Q80, Q80Q80, Q40Q40, Q41Q41,
  * Q80Q40} (core/GGMLComputeOps.kt:349-629), kind = lk_dot_kind: one dot, and every

@@ -71,6 +71,7 @@ def lib():
         L.lko_dequantize.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
         L.lko_compute_mat_mul.argtypes = [P, P, P]
         L.lko_compute_mat_mul_tight.argtypes = [P, P, P]
+        L.lko_compute_mat_mul_tight_mt.argtypes = [P, P, P, ctypes.c_int]
         L.lko_dot_direct.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.POINTER(ctypes.c_float)]
         L.lko_dot_direct_matrix.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, ctypes.c_void_p]
@@ -167,7 +168,8 @@ def last_error() -> str:
     return lib().lko_last_error().decode()
 
 
-def mat_mul_q(qtype: int, a_blocks: np.ndarray, M: int, K: int, x: np.ndarray, tight: bool = False) -> np.ndarray:
+def mat_mul_q(qtype: int, a_blocks: np.ndarray, M: int, K: int, x: np.ndarray, tight: bool = False,
+              threads: int = 1) -> np.ndarray:
     """Convenience: dst[M,N] = computeMatMul(A (qtype, ne=[K,M]), B (F32, ne=[N,K])).
 
     ``x`` is the B operand as a [K, N] float32 array (N fastest, as B.ne=[N,K] stores it).
@@ -184,7 +186,10 @@ def mat_mul_q(qtype: int, a_blocks: np.ndarray, M: int, K: int, x: np.ndarray, t
         a = make_tensor(qtype, [K, M], abuf)
     b = make_tensor(F32, [N, K], bbuf)
     d = make_tensor(F32, [N, M], dbuf)
-    st = (compute_mat_mul_tight if tight else compute_mat_mul)(a, b, d)
+    if tight and threads > 1:
+        st = lib().lko_compute_mat_mul_tight_mt(ctypes.byref(a), ctypes.byref(b), ctypes.byref(d), int(threads))
+    else:
+        st = (compute_mat_mul_tight if tight else compute_mat_mul)(a, b, d)
     _check(st)
     return dbuf.view(np.float32).reshape(M, N)
 
