@@ -233,6 +233,9 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_chain:
         result["decode_chain"] = decode_chain(torch, G, ga, nodes_by_layer, compute, token_bytes)
+        result["persistent_chain"] = {
+            "layer_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 1),
+            "decode_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 4)}
     if rank == 0 and world == 1 and not args.no_headline:
         result["headline_q4_0_4096x4096_n1"] = headline(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_batched:
@@ -320,6 +323,44 @@ def decode_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, reps=20):
     return {"tokens_per_s": round(1 / per, 2), "ms_per_token": round(per * 1e3, 4),
             "achieved_GBps": round(token_bytes / per / 1e9, 1), "launches_per_token": 4 * len(plans),
             "hip_graph": g is not None, "tokens_timed": reps}
+
+
+def persistent_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, per_layer, reps=20):
+    """The same token as ONE persistent launch (lk_plan_create_chain): per_layer groups of
+    dependent stages per layer (1: the 7 matrices of a layer as one stage, 32 stages; 4: the
+    decode schedule {q,k,v} -> o -> {gate,up} -> down, 128 stages), a device-side grid barrier
+    (agent-scope release / acquire) between consecutive stages, the next stage's weights
+    streaming while it completes. Captured in a HIP graph."""
+    groups = [tuple(n for (n, _, _) in LAYER_MATS)] if per_layer == 1 else CHAIN
+    nodes, stages = [], []
+    for layer, n in enumerate(nodes_by_layer):
+        for gi, grp in enumerate(groups):
+            for k in grp:
+                nodes.append(n[k])
+                stages.append(layer * len(groups) + gi)
+    plan = G.MulMatPlan(ga, nodes, stages=stages)
+
+    def token():
+        plan.launch(stream=stream)
+
+    with torch.cuda.stream(stream):
+        token()
+    torch.cuda.synchronize()
+    g = capture(torch, token, stream)
+    run = g.replay if g is not None else token
+    with torch.cuda.stream(stream):
+        run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            run()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    per = e0.elapsed_time(e1) / 1e3 / reps
+    timed_out = plan.timedOut()
+    return {"tokens_per_s": round(1 / per, 2), "ms_per_token": round(per * 1e3, 4),
+            "achieved_GBps": round(token_bytes / per / 1e9, 1), "stages_per_token": len(groups) * len(nodes_by_layer),
+            "launches_per_token": 1, "hip_graph": g is not None, "tokens_timed": reps, "barrier_timeout": timed_out}
 
 
 def headline(torch, G, dev, copies=48, reps=20):

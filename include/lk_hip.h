@@ -21,7 +21,9 @@
  *                         HIP stream (what GGMLBackend.graphCompute uses once operands
  *                         are resident; core/GGMLBackend.kt:146).
  *   lk_plan_*             core/GGMLBackend.kt:146 graphCompute(graph) over a graph whose
- *                         MUL_MAT nodes are mutually independent: one launch for the set.
+ *                         MUL_MAT nodes are mutually independent: one launch for the set;
+ *                         lk_plan_create_chain: a sequence of dependent stages of such nodes
+ *                         (computeGraph's node order, core/GGMLComputeOps.kt:2515) in one launch.
  *   lk_mul_mat_sharded    SURVEY §8b's sharded entry: computeMatMul with A's rows split
  *                         over the GPUs of one node from one host thread (the reference
  *                         is single-device; this is the north star's row sharding).
@@ -174,6 +176,18 @@ int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
 int lk_plan_launch(lk_plan *plan, void *stream);
 /* Number of kernel launches one lk_plan_launch issues. */
 int lk_plan_num_launches(const lk_plan *plan);
+/* A chain of DEPENDENT stages in one launch (a persistent streaming GEMV): node i belongs to
+ * stage stage[i] (0, then non-decreasing by at most 1). Stage s+1 starts only after every
+ * node of stage s has stored its outputs — a device-side grid barrier (agent-scope release /
+ * acquire) — so a stage may read what the previous one wrote; the next stage's weights are
+ * already streaming while the barrier completes. Same results as launching the stages' plans
+ * in order. Every node must be an N = 1 streaming-GEMV node of one quant type
+ * (LK_ERR_NOT_IMPLEMENTED otherwise). Launch with lk_plan_launch (graph-capturable). */
+int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage, int n,
+                         lk_plan **out);
+/* 1 if a chain launch gave up waiting at a barrier (its grid was not co-resident: results are
+ * then undefined) and re-arms the plan; 0 otherwise. Synchronizes the device. */
+int lk_plan_chain_timed_out(lk_plan *plan);
 void lk_plan_destroy(lk_plan *plan);
 
 /* ---- graph residency over host buffers ---------------------------------------

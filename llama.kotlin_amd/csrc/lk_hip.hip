@@ -1039,13 +1039,29 @@ struct lk_plan {
   std::vector<Group> groups;
   struct Single { lk_tensor a, b, d; Checked c; };
   std::vector<Single> singles;
+  unsigned *sync = nullptr;  // chain plans: barrier counters, exit counter, timeout flag
+  int nbar = 0;
 };
 
 namespace {
 
 // Workgroup g gets global rows [bound[g], bound[g+1]) of the concatenation of descs,
-// balanced by weight bytes, cut at node boundaries into work slots (spw per workgroup).
+// balanced by weight bytes, cut at node boundaries into segments.
+std::vector<std::vector<StreamWork>> split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid);
+
 void build_work(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<StreamWork> &work, int *spw) {
+  const auto per = split_rows(descs, qt, grid);
+  size_t most = 1;
+  for (auto &v : per) most = std::max(most, v.size());
+  *spw = (int)most;
+  work.assign((size_t)grid * most, StreamWork{});
+  for (int g = 0; g < grid; g++) {
+    for (size_t k = 0; k < per[g].size(); k++) work[(size_t)g * most + k] = per[g][k];
+    work[(size_t)g * most].count = (int32_t)per[g].size();
+  }
+}
+
+std::vector<std::vector<StreamWork>> split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid) {
   const int64_t pb = 2 * block_bytes(qt);
   const size_t n = descs.size();
   std::vector<int64_t> row0(n + 1, 0), byte0(n + 1, 0);
@@ -1065,7 +1081,6 @@ void build_work(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::v
     bound[g] = (g == grid) ? row0[n] : row0[i] + r;
   }
   std::vector<std::vector<StreamWork>> per(grid);
-  size_t most = 1;
   for (int g = 0; g < grid; g++) {
     for (size_t i = 0; i < n; i++) {
       const int64_t lo = std::max(bound[g], row0[i]), hi = std::min(bound[g + 1], row0[i + 1]);
@@ -1075,14 +1090,8 @@ void build_work(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::v
       w.K = descs[i].K; w.row_begin = (int32_t)(lo - row0[i]); w.row_end = (int32_t)(hi - row0[i]);
       per[g].push_back(w);
     }
-    most = std::max(most, per[g].size());
   }
-  *spw = (int)most;
-  work.assign((size_t)grid * most, StreamWork{});
-  for (int g = 0; g < grid; g++) {
-    for (size_t k = 0; k < per[g].size(); k++) work[(size_t)g * most + k] = per[g][k];
-    work[(size_t)g * most].count = (int32_t)per[g].size();
-  }
+  return per;
 }
 
 }  // namespace
@@ -1131,6 +1140,88 @@ int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
   return LK_OK;
 }
 
+// Chain plans: dependent stages in one launch of the streaming GEMV, one grid barrier per stage
+// boundary (gemv_stream_kernel's chain mode). One workgroup per CU, all co-resident (the
+// kernel's LDS admits one per CU).
+int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage, int n,
+                         lk_plan **out) {
+  if (!out || n <= 0 || !stage) return fail(LK_ERR_INVALID_ARG, "bad chain arguments");
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::vector<std::vector<GemvDesc>> stages;
+  int32_t qt = -1;
+  int cls = 0;
+  for (int i = 0; i < n; i++) {
+    if (stage[i] < 0 || (i > 0 && stage[i] < stage[i - 1]) || stage[i] > (i ? stage[i - 1] + 1 : 0))
+      return fail(LK_ERR_INVALID_ARG, "chain: stage ids must start at 0 and grow by at most 1 (node %d)", i);
+    Checked c;
+    if ((rc = check(&a[i], &b[i], &dst[i], &c))) return rc;
+    if (c.empty || !gemv_eligible(&a[i], &b[i], &dst[i], c) || !stream_class(&a[i], c))
+      return fail(LK_ERR_NOT_IMPLEMENTED, "chain: node %d is not a streaming GEMV node", i);
+    if (qt >= 0 && a[i].type != qt) return fail(LK_ERR_NOT_IMPLEMENTED, "chain: one quant type per chain");
+    qt = a[i].type;
+    cls = std::max(cls, stream_class(&a[i], c));
+    if ((int)stages.size() <= stage[i]) stages.emplace_back();
+    stages[stage[i]].push_back(make_desc(&a[i], &b[i], &dst[i], c));
+  }
+  const int grid = cu_count();
+  const int nbar = (int)stages.size() - 1;
+  auto plan = new lk_plan();
+  plan->nbar = nbar;
+  if (hipMalloc(&plan->sync, (nbar + 2) * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(plan->sync, 0, (nbar + 2) * sizeof(unsigned)) != hipSuccess) {
+    lk_plan_destroy(plan);
+    return fail(LK_ERR_DEVICE, "chain: sync alloc");
+  }
+  std::vector<std::vector<StreamWork>> per(grid);
+  for (size_t s = 0; s < stages.size(); s++) {
+    auto ps = split_rows(stages[s], qt, grid);
+    for (int g = 0; g < grid; g++) {
+      if (ps[g].empty()) {  // no rows here: the workgroup still takes part in the barrier
+        StreamWork w{};
+        w.a = stages[s][0].a; w.x = stages[s][0].x; w.dst = stages[s][0].dst; w.dst_row_stride = stages[s][0].dst_row_stride;
+        w.K = stages[s][0].K;
+        ps[g].push_back(w);
+      }
+      ps[g][0].barrier = (int32_t)s;  // barrier #s−1 before stage s (none before stage 0)
+      for (auto &w : ps[g]) per[g].push_back(w);
+    }
+  }
+  size_t most = 1;
+  for (auto &v : per) most = std::max(most, v.size());
+  std::vector<StreamWork> work((size_t)grid * most, StreamWork{});
+  for (int g = 0; g < grid; g++) {
+    for (size_t k = 0; k < per[g].size(); k++) {
+      per[g][k].nbar = nbar;
+      per[g][k].sync = plan->sync;
+      work[(size_t)g * most + k] = per[g][k];
+    }
+    work[(size_t)g * most].count = (int32_t)per[g].size();
+  }
+  void *dev = nullptr;
+  const size_t wb = work.size() * sizeof(StreamWork);
+  if (hipMalloc(&dev, wb) != hipSuccess) { lk_plan_destroy(plan); return fail(LK_ERR_DEVICE, "plan alloc"); }
+  plan->groups.push_back({qt, cls, grid, (int)most, (StreamWork *)dev});
+  if (hipMemcpy(dev, work.data(), wb, hipMemcpyHostToDevice) != hipSuccess) {
+    lk_plan_destroy(plan);
+    return fail(LK_ERR_DEVICE, "plan upload");
+  }
+  *out = plan;
+  return LK_OK;
+}
+
+int lk_plan_chain_timed_out(lk_plan *plan) {
+  if (!plan || !plan->sync) return 0;
+  unsigned flag = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(LK_ERR_DEVICE, "chain: sync");
+  if (hipMemcpy(&flag, plan->sync + plan->nbar + 1, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess) return fail(LK_ERR_DEVICE, "chain: flag");
+  if (flag) {
+    (void)hipMemset(plan->sync, 0, (plan->nbar + 2) * sizeof(unsigned));
+    return 1;
+  }
+  return 0;
+}
+
 int lk_plan_launch(lk_plan *plan, void *stream) {
   if (!plan) return fail(LK_ERR_INVALID_ARG, "null plan");
   hipStream_t st = pick_stream(stream);
@@ -1152,6 +1243,7 @@ int lk_plan_num_launches(const lk_plan *plan) {
 void lk_plan_destroy(lk_plan *plan) {
   if (!plan) return;
   for (auto &g : plan->groups) (void)hipFree(g.work);
+  if (plan->sync) (void)hipFree(plan->sync);
   delete plan;
 }
 

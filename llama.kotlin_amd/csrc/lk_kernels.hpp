@@ -296,7 +296,10 @@ struct StreamWork {
   float *dst;
   int64_t dst_row_stride;
   int32_t K, row_begin, row_end, count;
-  int64_t pad[2];
+  // chain plans (lk_plan_create_chain): barrier > 0 puts grid barrier #barrier−1 before this
+  // segment; sync = [nbar] arrival counters, [nbar] exit counter, [nbar + 1] timeout flag
+  int32_t barrier, nbar;
+  unsigned *sync;
 };
 static_assert(sizeof(StreamWork) == 64, "one s_load_dwordx16");
 
@@ -436,12 +439,14 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
   LK_TRACE(0);
   const StreamWork *wk = work ? work + (int64_t)blockIdx.x * spw : nullptr;
   const int nseg = wk ? ((const __attribute__((address_space(4))) int32_t *)wk)[offsetof(StreamWork, count) / 4] : 1;
+  int nbar = 0;
+  unsigned *sync = nullptr;
   for (int si = 0; si < nseg; si++) {
     const uint8_t *a_node;
     const float *x_node;
     float *dst_node;
     int64_t dst_stride;
-    int K, rb, re;
+    int K, rb, re, bar = 0;
     if (wk) {
       StreamWork w;  // scalar loads (constant address space: the work list is never written)
       {
@@ -453,6 +458,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       }
       a_node = w.a; x_node = w.x; dst_node = w.dst; dst_stride = w.dst_row_stride;
       K = w.K; rb = w.row_begin; re = w.row_end;
+      bar = w.barrier; nbar = w.nbar; sync = w.sync;
     } else {
       a_node = single.a; x_node = single.x; dst_node = single.dst; dst_stride = single.dst_row_stride;
       K = single.K;
@@ -519,29 +525,66 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(xv + p * 16 + t), (LK_LDS void *)(lds + k * 64), 16, 0, 0);
       }
     };
+    auto weight_prologue = [&](bool with_x) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < G::D; k++) {
+        if (with_x && LK_PROLOGUE_ORDER == 1 && k == 1) dma_x();
+        const bool real = k < nunits;
+        const LK_GLOBAL uint8_t *base = real ? A + (int64_t)irow * RB + (int64_t)ich * G::UB : (const LK_GLOBAL uint8_t *)a_node;
+        const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : (int)min((int64_t)G::UB, RB);
+        dma_unit(base, ubytes, k);
+        if (real) {
+          if (++ich == nch) { ich = 0; ++irow; }
+          ++issued;
+        }
+      }
+      islot = 0;  // the next unit to issue is unit D, slot D % D
+    };
+    if (bar) {
+      // chain plans: grid barrier #bar−1 between dependent stages, inside the launch.
+      // 1. this workgroup's stores of the previous stage have completed; one lane releases
+      //    them (L2 write-back) and arrives
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (wave == 0 && lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(sync + bar - 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // 2. the weights do not depend on the previous stage: their stream starts now
+      weight_prologue(false);
+      // 3. one lane waits for every workgroup (bounded: a grid that is not co-resident sets the
+      //    timeout flag and runs on instead of hanging), then acquires for the whole CU
+      if (wave == 0 && lane == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(sync + bar - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+          __builtin_amdgcn_s_sleep(2);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 200 ms at 100 MHz
+            __hip_atomic_store(sync + nbar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      // 4. the stage's activations (the youngest DMA: wait for everything)
+      dma_x();
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+    } else {
     if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
     if (LK_PROLOGUE_ORDER == 0 || LK_PROLOGUE_ORDER == 2) dma_x();
     if (LK_PROLOGUE_ORDER == 2) {  // the image first, alone: its latency is not queued behind the weight burst
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
     }
-#pragma unroll
-    for (int k = 0; k < G::D; k++) {
-      if (LK_PROLOGUE_ORDER == 1 && k == 1) dma_x();
-      const bool real = k < nunits;
-      const LK_GLOBAL uint8_t *base = real ? A + (int64_t)irow * RB + (int64_t)ich * G::UB : (const LK_GLOBAL uint8_t *)a_node;
-      const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : (int)min((int64_t)G::UB, RB);
-      dma_unit(base, ubytes, k);
-      if (real) {
-        if (++ich == nch) { ich = 0; ++irow; }
-        ++issued;
-      }
-    }
-    islot = 0;  // the next unit to issue is unit D, slot D % D
+    weight_prologue(true);
 
     if (LK_PROLOGUE_ORDER != 2) {
       wait_vmcnt<(LK_PROLOGUE_ORDER == 0 ? G::D : G::D - 1) * G::L>();  // this wave's activation DMA has landed
       __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    }
     }
 
     // 2. activations into VGPRs in decode order, and Σx per block
@@ -609,6 +652,18 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       const float tot = dpp_sum(acc);
 #endif
       if (lane == 63) out[(int64_t)row * dst_stride] = tot;
+    }
+  }
+  if (sync) {
+    // chain plans: the workgroup that leaves last (every workgroup has passed every barrier)
+    // re-arms the counters for the next launch (stream order makes the stores visible to it)
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (wave == 0 && lane == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(sync + nbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1) {
+        for (int b = 0; b <= nbar; b++) __hip_atomic_store(sync + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   LK_TRACE(3);

@@ -74,7 +74,8 @@ def raise_for_status(status: int, msg: str):
 EXPORTED_SYMBOLS = (
     "lk_init", "lk_device_count", "lk_last_error", "lk_shutdown", "lk_version",
     "lk_mul_mat_validate", "lk_mul_mat", "lk_mul_mat_device", "lk_mul_mat_sharded", "lk_weights_pin_sharded",
-    "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy",
+    "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy", "lk_plan_create_chain",
+    "lk_plan_chain_timed_out",
     "lk_graph_create", "lk_graph_compute", "lk_graph_num_levels", "lk_graph_num_launches",
     "lk_graph_transfer_bytes", "lk_graph_destroy",
     "lk_weights_pin", "lk_weights_evict_all", "lk_weights_cached_bytes",
@@ -118,6 +119,8 @@ def load():
     L.lk_weights_pin_sharded.argtypes = [P, ctypes.c_uint64, ctypes.c_int]
     L.lk_plan_create.argtypes = [P, P, P, ctypes.c_int, ctypes.POINTER(vp)]
     L.lk_plan_launch.argtypes = [vp, vp]
+    L.lk_plan_create_chain.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.POINTER(vp)]
+    L.lk_plan_chain_timed_out.argtypes = [vp]
     L.lk_plan_num_launches.argtypes = [vp]
     L.lk_plan_destroy.argtypes = [vp]
     L.lk_plan_destroy.restype = None

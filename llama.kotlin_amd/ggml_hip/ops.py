@@ -124,7 +124,11 @@ class MulMatPlan:
     (GGMLBackend.graphCompute over such a graph, core/GGMLBackend.kt:146): nodes of
     one quant type share a single grouped kernel launch."""
 
-    def __init__(self, ga: GGMLGraphAllocator, nodes):
+    def __init__(self, ga: GGMLGraphAllocator, nodes, stages=None):
+        """stages: None — the nodes are mutually independent (lk_plan_create); or one stage id
+        per node (0, non-decreasing) — a chain of dependent stages in one persistent launch with
+        a device-side grid barrier between stages (lk_plan_create_chain): stage s+1 may read
+        what stage s wrote."""
         L = _lib.load()
         n = len(nodes)
         A = (_lib.LkTensor * max(n, 1))()
@@ -133,8 +137,22 @@ class MulMatPlan:
         for i, (a, b, d) in enumerate(nodes):
             A[i], B[i], D[i] = to_lk(ga, a), to_lk(ga, b), to_lk(ga, d)
         self._handle = ctypes.c_void_p()
-        _lib.check(L.lk_plan_create(A, B, D, n, ctypes.byref(self._handle)))
-        self._keep = (A, B, D)
+        if stages is None:
+            _lib.check(L.lk_plan_create(A, B, D, n, ctypes.byref(self._handle)))
+            S = None
+        else:
+            if len(stages) != n:
+                raise _lib.IllegalArgumentException("one stage id per node")
+            S = (ctypes.c_int32 * max(n, 1))(*[int(v) for v in stages])
+            _lib.check(L.lk_plan_create_chain(A, B, D, S, n, ctypes.byref(self._handle)))
+        self._keep = (A, B, D, S)
+
+    def timedOut(self) -> bool:
+        """Chain plans: True if a launch gave up waiting at a barrier (grid not co-resident)."""
+        st = _lib.load().lk_plan_chain_timed_out(self._handle)
+        if st < 0 or st > 1:
+            _lib.check(st)
+        return st == 1
 
     @property
     def numLaunches(self) -> int:
