@@ -1813,10 +1813,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restr
   if (idx >= (int64_t)M * c4) return;
   const int64_t m = idx / c4;
   const int n0 = (int)(idx % c4) * 4;
+  // slabs in slice order (deterministic); eight loads in flight at a time instead of one
+  // dependent L2 round trip per slice
   f32x4 s = *(const f32x4 *)(P + m * N16 + n0);
-  for (int sl = 1; sl < slices; sl++) {
-    const f32x4 v = *(const f32x4 *)(P + ((int64_t)sl * M + m) * N16 + n0);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  for (int b = 1; b < slices; b += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      if (b + i < slices) v[i] = *(const f32x4 *)(P + ((int64_t)(b + i) * M + m) * N16 + n0);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      if (b + i < slices) { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
   }
   const float e4[4] = {s.x, s.y, s.z, s.w};
   if (d_nb0 == 4 && n0 + 4 <= N && (((uintptr_t)(dst + m * d_nb1 + n0 * 4)) & 15) == 0) {
