@@ -1047,10 +1047,11 @@ namespace {
 
 // Workgroup g gets global rows [bound[g], bound[g+1]) of the concatenation of descs,
 // balanced by weight bytes, cut at node boundaries into segments.
-std::vector<std::vector<StreamWork>> split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid);
+void split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<std::vector<StreamWork>> &per);
 
 void build_work(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<StreamWork> &work, int *spw) {
-  const auto per = split_rows(descs, qt, grid);
+  std::vector<std::vector<StreamWork>> per;
+  split_rows(descs, qt, grid, per);
   size_t most = 1;
   for (auto &v : per) most = std::max(most, v.size());
   *spw = (int)most;
@@ -1061,7 +1062,7 @@ void build_work(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::v
   }
 }
 
-std::vector<std::vector<StreamWork>> split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid) {
+void split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<std::vector<StreamWork>> &per) {
   const int64_t pb = 2 * block_bytes(qt);
   const size_t n = descs.size();
   std::vector<int64_t> row0(n + 1, 0), byte0(n + 1, 0);
@@ -1080,7 +1081,7 @@ std::vector<std::vector<StreamWork>> split_rows(const std::vector<GemvDesc> &des
     r = std::min<int64_t>(std::max<int64_t>(r, 0), descs[i].M);
     bound[g] = (g == grid) ? row0[n] : row0[i] + r;
   }
-  std::vector<std::vector<StreamWork>> per(grid);
+  per.assign(grid, {});
   for (int g = 0; g < grid; g++) {
     for (size_t i = 0; i < n; i++) {
       const int64_t lo = std::max(bound[g], row0[i]), hi = std::min(bound[g + 1], row0[i + 1]);
@@ -1091,7 +1092,6 @@ std::vector<std::vector<StreamWork>> split_rows(const std::vector<GemvDesc> &des
       per[g].push_back(w);
     }
   }
-  return per;
 }
 
 }  // namespace
@@ -1175,7 +1175,8 @@ int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor
   }
   std::vector<std::vector<StreamWork>> per(grid);
   for (size_t s = 0; s < stages.size(); s++) {
-    auto ps = split_rows(stages[s], qt, grid);
+    std::vector<std::vector<StreamWork>> ps;
+    split_rows(stages[s], qt, grid, ps);
     for (int g = 0; g < grid; g++) {
       if (ps[g].empty()) {  // no rows here: the workgroup still takes part in the barrier
         StreamWork w{};

@@ -11,7 +11,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblk_hip.so")
+LIB_PATH = os.environ.get("LK_HIP_LIB") or os.path.join(HERE, "liblk_hip.so")  # env: lab A/B builds only
 
 # status codes (include/lk_hip.h)
 LK_OK = 0
