@@ -506,6 +506,35 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
   return LK_OK;
 }
 
+// gemm_skinny_pair_kernel: the same split-K tasks, a wave pair per stream (8 waves).
+template <int QT, int NT>
+int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
+  using SG = SkinnyPairGeom<QT, NT>;
+  GemmScratch &S = gemm_scratch();
+  const int nblk = g.K / 32;
+  const int slices = (nblk + SG::SB - 1) / SG::SB;
+  const int ntile = (g.M + 15) / 16;
+  int ranges = std::max(1, std::min(ntile, (cu_count() + slices - 1) / slices));
+  g.tiles_per_range = (ntile + ranges - 1) / ranges;
+  ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
+  g.slices = slices;
+  if (slices > 1) {
+    const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
+    if (rc) return rc;
+    g.partial = (float *)S.partial;
+  }
+  g.tasks = ranges * slices;
+  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  hipLaunchKernelGGL((gemm_skinny_pair_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
+  if (slices > 1) {
+    const int64_t threads = (int64_t)g.M * (16 * NT / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
+                       slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
 int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   SkinnyArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
@@ -515,6 +544,12 @@ int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
   const bool one = c.N <= 16;
+  static const int pair = [] { const char *e = getenv("LK_SKINNY_PAIR"); return e ? atoi(e) : 1; }();  // A/B
+  if (pair && (!one || pair == 2)) switch (a->type) {  // LK_SKINNY_PAIR=2: N <= 16 too (lab)
+    case LK_TYPE_Q4_0: return one ? launch_skinny_pair_t<LK_TYPE_Q4_0, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_0, 2>(g, st);
+    case LK_TYPE_Q4_1: return one ? launch_skinny_pair_t<LK_TYPE_Q4_1, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_1, 2>(g, st);
+    default: break;
+  }
   switch (a->type) {
     case LK_TYPE_Q4_0: return one ? launch_skinny_t<LK_TYPE_Q4_0, 1>(g, st) : launch_skinny_t<LK_TYPE_Q4_0, 2>(g, st);
     case LK_TYPE_Q4_1: return one ? launch_skinny_t<LK_TYPE_Q4_1, 1>(g, st) : launch_skinny_t<LK_TYPE_Q4_1, 2>(g, st);

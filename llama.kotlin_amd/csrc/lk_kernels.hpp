@@ -1514,6 +1514,281 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
 #undef LK_STRACE
 }
 
+// ---- skinny GEMM on wave pairs (Q4_0 / Q4_1, 17 <= N <= 32) -------------------------------
+//
+// gemm_skinny_kernel runs one wave per SIMD (all of the slice's x-fragments, 256 VGPRs at
+// N 32): a lone wave issues VALU every 4 cycles and nothing overlaps its MFMAs. Here the
+// slice's 16 blocks are split over a wave pair on one SIMD: wave (stream p = w % 4, half
+// h = w / 4) holds x for blocks [8h, 8h + 8) (128 VGPRs), streams its half of each row piece
+// through its own LDS-DMA ring and computes that half's partial dot. The h = 1 wave hands its
+// accumulators to its partner through LDS (two parities), behind a ready flag; the partner adds
+// them in a fixed order (deterministic) and stores, then acknowledges. No workgroup barrier
+// after the prologue: each pair runs at its own pace.
+template <int QT, int NT> struct SkinnyPairGeom {
+  static constexpr int NW = 8;                          // 4 streams x 2 halves
+  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr int SB = 16, SBH = 8;                // blocks per slice / per half
+  static constexpr int RPH = SBH * BB;                  // bytes of a half row piece (multiple of 16)
+  static constexpr int PPH = RPH / 16;                  // 16-B cells per half row
+  static constexpr int L = (16 * PPH + 63) / 64;        // DMA instructions per half unit
+  static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
+  static constexpr int SLOT = L * 1024;
+  static constexpr int XB = SB * NT * kXSplits * 1024;  // activation fragments (staging)
+  static constexpr int TB = QT == LK_TYPE_Q4_1 ? SB * NT * 16 * 4 : 0;  // Σx per (block, column)
+  static constexpr int EB = 2 * 4 * NT * 64 * 16;       // accumulator hand-off, 2 parities x 4 pairs
+  static constexpr int FB = 64;                         // ready[4][2], ack[4] (ints)
+  static constexpr int DFIT = (kLdsBytes - XB - TB - EB - FB) / (NW * SLOT);
+  static constexpr int D = DFIT > 3 ? 3 : DFIT;         // ring depth (half units per wave)
+  static constexpr int LDS = XB + TB + EB + FB + NW * D * SLOT;
+  static constexpr int FPW = SB * NT / NW;              // fragments each wave converts
+  static constexpr int MAXW = L * (D - 1) + D * NT;     // largest vmcnt a wait needs
+  static_assert(RPH % 16 == 0, "half row pieces");
+  static_assert(D >= 2, "ring must double-buffer");
+  static_assert(LDS <= kLdsBytes, "LDS");
+  static_assert((SB * NT) % NW == 0, "fragments per wave");
+  static_assert(MAXW < 64, "vmcnt");
+};
+
+// s_waitcnt vmcnt(x) for a wave-uniform run-time x in [0, J] (x > J waits for J).
+template <int J> __device__ __forceinline__ void wait_vmcnt_rt(int x) {
+  if constexpr (J == 0) wait_vmcnt<0>();
+  else if (x >= J) wait_vmcnt<J>();
+  else wait_vmcnt_rt<J - 1>(x);
+}
+
+// Block B (0..7) of this wave's half: x held as [8][NT]; T (Q4_1) indexed by the slice block.
+template <int QT, int NT, int B, int WPB>
+__device__ __forceinline__ void skinny_pair_block(const uint32_t (&w)[WPB], const float *tl, int lane, const u32x4 (&xh)[8][NT],
+                                                  const u32x4 (&xl)[8][NT], f32x4 (&acc)[NT]) {
+  constexpr int OB = B * QTraits<QT>::BB;
+  bf16x8 wf;
+  float s1, s2 = 0.f;
+  if constexpr (QT == LK_TYPE_Q4_1) {
+    wf = Q4Frag<0>::make(w[1]);
+    s1 = 512.f * h2f(w[0]);
+    s2 = h2f(w[0] >> 16);
+  } else if constexpr (QT == LK_TYPE_Q4_0) {
+    if constexpr ((OB & 3) == 0) {
+      wf = q4_0_frag_biased(align2(w[2], w[1]));
+      s1 = 512.f * h2f(w[0]);
+    } else {
+      wf = q4_0_frag_biased(w[1]);
+      s1 = 512.f * h2f(w[0] >> 16);
+    }
+  } else {
+    if constexpr ((OB & 3) == 0) {
+      wf = w_frag<LK_TYPE_Q8_0>(align2(w[2], w[1]), align2(w[3], w[2]));
+      s1 = h2f(w[0]);
+    } else {
+      wf = w_frag<LK_TYPE_Q8_0>(w[1], w[2]);
+      s1 = h2f(w[0] >> 16);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf, f32x4{0.f, 0.f, 0.f, 0.f},
+                                                      0, 0, 0);
+    p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (QT == LK_TYPE_Q4_1) t = *(const f32x4 *)(tl + (B * NT + j) * 16 + (lane >> 4) * 4);
+    accumulate_s<QT == LK_TYPE_Q4_1>(acc[j], s1, s2, p, t);
+  }
+}
+
+template <int QT, int NT, int WPB, bool FULL, int B>
+__device__ __forceinline__ void skinny_pair_blocks(const uint32_t (&w)[8][WPB], const float *tl, int nb, int lane,
+                                                   const u32x4 (&xh)[8][NT], const u32x4 (&xl)[8][NT], f32x4 (&acc)[NT]) {
+  if constexpr (B < 8) {
+    if (!FULL && B >= nb) return;
+    skinny_pair_block<QT, NT, B, WPB>(w[B], tl, lane, xh, xl, acc);
+    skinny_pair_blocks<QT, NT, WPB, FULL, B + 1>(w, tl, nb, lane, xh, xl, acc);
+  }
+}
+
+// LDS flags between the two waves of a pair. LDS serves one wave's requests in order, so a
+// flag written after the data is seen after it; the compiler barriers keep the source order
+// (a workgroup-scope atomic would also order the wave's in-flight DMA, which is not needed).
+__device__ __forceinline__ int lds_ld(const int *p) {
+  asm volatile("" ::: "memory");
+  const int v = *(volatile const LK_LDS int *)(LK_LDS const int *)p;
+  asm volatile("" ::: "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_st(int *p, int v) {
+  asm volatile("" ::: "memory");
+  *(volatile LK_LDS int *)(LK_LDS int *)p = v;
+  asm volatile("" ::: "memory");
+}
+
+template <int QT, int NT>
+__global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
+  using G = SkinnyPairGeom<QT, NT>;
+  constexpr int BB = G::BB, D = G::D, L = G::L, NW = G::NW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t *xlds = smem;
+  float *tlds = (float *)(smem + G::XB);
+  f32x4 *xch = (f32x4 *)(smem + G::XB + G::TB);
+  int *flags = (int *)(smem + G::XB + G::TB + G::EB);  // ready[p][parity] at 2p + parity, ack[p] at 8 + p
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int p = wave & 3, h = wave >> 2;
+  uint8_t *ring = smem + G::XB + G::TB + G::EB + G::FB + wave * D * G::SLOT;
+  // XCD-aware task order, as gemm_skinny_kernel
+  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+  if (task >= g.tasks) return;  // grid padding (before any barrier: the whole workgroup leaves)
+  if (threadIdx.x < 16) flags[threadIdx.x] = 0;  // published by the prologue's barrier
+  const int slice = task % g.slices, range = task / g.slices;
+  const int nblk = g.K / 32;
+  const int kb0 = slice * G::SB, nb = min(G::SB, nblk - kb0);
+  const int nbh = max(0, min(G::SBH, nb - G::SBH * h));  // this wave's blocks (a short slice may leave h = 1 none)
+  const int64_t RB = (int64_t)nblk * BB;
+  const int ntile = (g.M + 15) / 16;
+  const int t0 = range * g.tiles_per_range, t1 = min(t0 + g.tiles_per_range, ntile);
+  const int nunits = t1 - t0 - p > 0 ? (t1 - t0 - p + 3) / 4 : 0;  // stream p: tiles t0 + p + 4i
+  const int pph = nbh * BB / 16;
+  const int myL = nbh > 0 ? L : 0;
+
+  // half unit u = rows of tile t0 + p + 4u, bytes [kb0·BB + h·RPH, + nbh·BB) of each; cell
+  // q = r·PPH + c lands at slot + 16q (row pitch RPH); cells past the unit re-read cell 0
+  const uint8_t *abase = g.a + (int64_t)kb0 * BB + (int64_t)h * G::RPH;
+  uint32_t rofs[L];
+  int rrow[L];
+#pragma unroll
+  for (int j = 0; j < L; j++) {
+    const int q = j * 64 + lane, r = q / G::PPH, c = q % G::PPH;
+    rrow[j] = min(r, 15);
+    rofs[j] = (uint32_t)((c < pph && r < 16) ? c * 16 : 0);
+  }
+  auto issue = [&](int u, int sl) __attribute__((always_inline)) {
+    const int t = t0 + p + u * 4;
+    const uint8_t *tb = abase + (int64_t)t * 16 * RB;
+    const int rmax = g.M - 1 - t * 16;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
+      dma16<LK_SKINNY_NT>(tb, vofs, ring + sl * G::SLOT + j * 1024);
+    }
+  };
+
+  // 1. activations of the slice -> LDS fragments, as gemm_skinny_kernel (compiler-visible loads:
+  //    issued before the weight ring, so waiting for them never waits for it)
+  float v[G::FPW][8];
+#pragma unroll
+  for (int i = 0; i < G::FPW; i++) {
+    const int f = wave + i * NW, b = f / NT, j = f % NT;
+    const int n = 16 * j + (lane & 15);
+    const int64_t k0 = 32 * (int64_t)(kb0 + b) + 8 * (lane >> 4);
+    const bool ok = b < nb && n < g.N;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int kk = (QT != LK_TYPE_Q8_0) ? ((e & 3) * 2 + (e >> 2)) : e;
+      v[i][e] = ok ? *(const float *)(g.b + n * g.b_nb0 + (k0 + kk) * g.b_nb1) : 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < G::FPW; i++) {
+    const int f = wave + i * NW;
+    float part = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; e++) part += v[i][e];
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      uint32_t hh[2], ll[2];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t bx = __builtin_bit_cast(uint32_t, v[i][e + q]);
+        const float r = v[i][e + q] - __builtin_bit_cast(float, bx & 0xFFFF0000u);  // exact
+        uint32_t br = __builtin_bit_cast(uint32_t, r);
+        br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even
+        hh[q] = bx;
+        ll[q] = br;
+      }
+      hi[e / 2] = __builtin_amdgcn_perm(hh[1], hh[0], 0x07060302u);
+      lo[e / 2] = __builtin_amdgcn_perm(ll[1], ll[0], 0x07060302u);
+    }
+    u32x4 *xf = (u32x4 *)(xlds + (f * kXSplits) * 1024) + lane;
+    xf[0] = u32x4{hi[0], hi[1], hi[2], hi[3]};
+    xf[64] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+    if constexpr (QT == LK_TYPE_Q4_1) {
+      part += __shfl_xor(part, 16, kWave);
+      part += __shfl_xor(part, 32, kWave);
+      if (lane < 16) tlds[f * 16 + lane] = part;
+    }
+  }
+  // 2. the weight ring
+  if (myL)
+    for (int u = 0; u < min(D, nunits); u++) issue(u, u);
+  wait_lgkmcnt0();
+  __builtin_amdgcn_s_barrier();  // fragments and flags visible (bare: the ring stays in flight)
+  // 3. this wave holds the fragments of its 8 blocks
+  u32x4 xh[8][NT], xl[8][NT];
+#pragma unroll
+  for (int b = 0; b < 8; b++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int bb = min(8 * h + b, G::SB - 1);
+      const u32x4 *xf = (const u32x4 *)(xlds + ((bb * NT + j) * kXSplits) * 1024) + lane;
+      xh[b][j] = xf[0];
+      xl[b][j] = xf[64];
+    }
+  const float *tl = tlds + 8 * h * NT * 16;
+
+  const int N16 = 16 * NT;
+  const int SH = h == 0 ? NT : 0;  // stores per unit (at least; slices == 1 may store more)
+  for (int u = 0; u < nunits; u++) {
+    const int slot = u % D;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (myL) {
+      // ops younger than this unit's DMA: its successors already issued, and the stores since
+      wait_vmcnt_rt<G::MAXW>(myL * min(D - 1, nunits - 1 - u) + min(u, D) * SH);
+      asm volatile("" ::: "memory");
+      uint32_t wd[8][G::WPB];
+      {
+        const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::RPH;
+        const uint8_t *bg = bm + (QT == LK_TYPE_Q8_0 ? 8 : 4) * (lane >> 4);
+        skinny_read_all<QT, 8, G::WPB, 0>(bm, bg, wd);
+        asm volatile("" ::: "memory");
+      }
+      if (nbh == 8) skinny_pair_blocks<QT, NT, G::WPB, true, 0>(wd, tl, nbh, lane, xh, xl, acc);
+      else skinny_pair_blocks<QT, NT, G::WPB, false, 0>(wd, tl, nbh, lane, xh, xl, acc);
+      wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
+      if (u + D < nunits) issue(u + D, slot);
+    }
+    f32x4 *xb = xch + ((u & 1) * 4 + p) * NT * 64 + lane;
+    if (h == 1) {
+      // the partner has consumed unit u − 2 (this parity's previous contents)
+      while (lds_ld(flags + 8 + p) < u - 1) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int j = 0; j < NT; j++) xb[j * 64] = acc[j];
+      lds_st(flags + 2 * p + (u & 1), u + 1);
+    } else {
+      while (lds_ld(flags + 2 * p + (u & 1)) != u + 1) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int j = 0; j < NT; j++) acc[j] += xb[j * 64];
+      lds_st(flags + 8 + p, u + 1);
+      // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
+      const int t = t0 + p + u * 4;
+      const int64_t m = (int64_t)t * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NT; j++) {
+        const int n0 = 16 * j + 4 * (lane >> 4);
+        if (g.slices > 1) {
+          if (m < g.M) *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = acc[j];
+        } else if (m < g.M) {
+          const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+        }
+      }
+    }
+  }
+  wait_vmcnt<0>();
+}
+
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------
 //
 // MFMA-bound once N is large, but the activation operand costs 4 B per element (bf16 hi + lo),
