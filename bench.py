@@ -239,6 +239,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_headline:
         result["headline_q4_0_4096x4096_n1"] = headline(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_batched:
+        result["n1_configs"] = n1_configs(torch, G, dev)
         result["batched"] = batched(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_host_path:
         result["host_path_pcie"] = host_path(torch, G, dev)
@@ -415,6 +416,60 @@ def headline(torch, G, dev, copies=48, reps=20):
                                          "frac_of_8TBps": round(gbs_g / HBM_PEAK_GBS, 4)}}
 
 
+BLOCK_BYTES = {"Q4_0": 18, "Q4_1": 20, "Q8_0": 34}
+
+
+def n1_configs(torch, G, dev, reps=20):
+    """BASELINE.json configs at batch 1 beside the headline: C2 (Q8_0 4096x4096) and C3's FFN
+    shapes (Q4_0 / Q4_1 11008x4096 and 4096x11008), one computeMatMul launch per matrix over
+    rotating weight copies (> Infinity Cache), graph-replayed; algorithmic GB/s."""
+    T = G.GGMLType
+    out = {}
+    for name, qn, M, K, copies in (("c2_q8_0_4096x4096_n1", "Q8_0", 4096, 4096, 32),
+                                   ("c3_q4_0_11008x4096_n1", "Q4_0", 11008, 4096, 16),
+                                   ("c3_q4_1_11008x4096_n1", "Q4_1", 11008, 4096, 16),
+                                   ("c3_q4_0_4096x11008_n1", "Q4_0", 4096, 11008, 16)):
+        qt = getattr(T, qn)
+        nb = M * K // 32 * BLOCK_BYTES[qn]
+        nb16 = (nb + 15) // 16 * 16
+        g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+        wb = g.addBuffer(copies * nb16 + 256)
+        xb = g.addBuffer(4 * K + 256)
+        db = g.addBuffer(4 * M * copies + 256)
+        src = torch.randn(M * K, device=dev) * 0.02
+        for c in range(copies):
+            g.buffers[wb][c * nb16:c * nb16 + nb].copy_(G.quantizeTensor(src * (1 + 0.01 * c), qt))
+        g.buffers[xb][: 4 * K].copy_(torch.randn(K, device=dev).view(torch.uint8))
+        nodes = [(G.GGMLTensor(qt, [K, M], bufferId=wb, dataOffset=c * nb16), G.GGMLTensor(T.F32, [1, K], bufferId=xb),
+                  G.GGMLTensor(T.F32, [1, M], bufferId=db, dataOffset=4 * M * c)) for c in range(copies)]
+        s = torch.cuda.Stream(device=dev)
+
+        def run_all():
+            for (a, b, d) in nodes:
+                G.computeMatMul(g, None, a, b, d, stream=s)
+
+        with torch.cuda.stream(s):
+            run_all()
+        torch.cuda.synchronize()
+        gr = capture(torch, run_all, s)
+        fn = gr.replay if gr is not None else run_all
+        with torch.cuda.stream(s):
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
+                fn()
+            e1.record(s)
+        torch.cuda.synchronize()
+        per = e0.elapsed_time(e1) / 1e3 / (reps * copies)
+        nbytes = nb + 4 * K + 4 * M
+        out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
+                     "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
+                     "rotating_weight_copies": copies, "hip_graph": gr is not None}
+        del g
+    return out
+
+
 def batched(torch, G, dev, reps=10):
     """SURVEY §8d configs C3 (Q4_0 11008x4096, N = 32: HBM-bound) and C5 (Q4_0 4096x4096, N = 512:
     MFMA-bound) through computeMatMul (xsplit_kernel + gemm_q_lds_kernel), one call per matrix,
@@ -423,17 +478,20 @@ def batched(torch, G, dev, reps=10):
     x = hi + lo)."""
     T = G.GGMLType
     out = {}
-    for name, M, K, N, copies in (("c3_q4_0_11008x4096_n32", 11008, 4096, 32, 16), ("c5_q4_0_4096x4096_n512", 4096, 4096, 512, 32)):
-        nb = M * K // 32 * Q4_0_BLOCK
+    for name, qn, M, K, N, copies in (("c3_q4_0_11008x4096_n32", "Q4_0", 11008, 4096, 32, 16),
+                                      ("c3_q4_1_11008x4096_n32", "Q4_1", 11008, 4096, 32, 16),
+                                      ("c5_q4_0_4096x4096_n512", "Q4_0", 4096, 4096, 512, 32)):
+        qt = getattr(T, qn)
+        nb = M * K // 32 * BLOCK_BYTES[qn]
         g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
         wb = g.addBuffer(copies * nb + 256)
         xb = g.addBuffer(4 * K * N + 256)
         db = g.addBuffer(4 * M * N * copies + 256)
         src = torch.randn(M * K, device=dev) * 0.02
         for c in range(copies):
-            g.buffers[wb][c * nb:(c + 1) * nb].copy_(G.quantizeTensor(src * (1 + 0.01 * c), T.Q4_0))
+            g.buffers[wb][c * nb:(c + 1) * nb].copy_(G.quantizeTensor(src * (1 + 0.01 * c), qt))
         g.buffers[xb][: 4 * K * N].copy_(torch.randn(K * N, device=dev).view(torch.uint8))
-        nodes = [(G.GGMLTensor(T.Q4_0, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [N, K], bufferId=xb),
+        nodes = [(G.GGMLTensor(qt, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [N, K], bufferId=xb),
                   G.GGMLTensor(T.F32, [N, M], bufferId=db, dataOffset=4 * M * N * c)) for c in range(copies)]
         s = torch.cuda.Stream(device=dev)
 
@@ -455,7 +513,7 @@ def batched(torch, G, dev, reps=10):
             e1.record(s)
         torch.cuda.synchronize()
         per = e0.elapsed_time(e1) / 1e3 / (reps * copies)
-        nbytes = alg_bytes(M, K, N)
+        nbytes = nb + 4 * K * N + 4 * M * N
         tf = 2 * M * N * K / per / 1e12
         out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
                      "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "useful_TFLOPs": round(tf, 2),
@@ -581,6 +639,16 @@ def cpu_baseline(sample_rows, token_bytes, min_seconds=10.0):
         variants[label] = {"value": round(g, 4), "unit": "GB/s", "cores": nthr, "tokens_per_s": round(g * 1e9 / token_bytes, 4),
                            "sample": f"{'all rows' if rows_cap is None else f'first {rows_cap} rows'} of each layer matrix, "
                                      f"{tb} algorithmic bytes, {tt:.2f} s"}
+    # config C2's CPU side ("Kotlin CPU vecDotQ8_0"): the structural restatement on Q8_0 4096x4096
+    rows = 4096
+    q = O.quantize(O.Q8_0, (rng.standard_normal(rows * 4096) * 0.02).astype(np.float32))
+    x = rng.standard_normal((4096, 1)).astype(np.float32)
+    t0 = time.perf_counter()
+    O.mat_mul_q(O.Q8_0, q, rows, 4096, x)
+    tq = time.perf_counter() - t0
+    qb = rows * 4096 // 32 * 34 + 4 * 4096 + 4 * rows
+    variants["structural_q8_0_4096x4096"] = {"value": round(qb / tq / 1e9, 5), "unit": "GB/s", "cores": 1,
+                                             "sample": f"{rows} rows of a Q8_0 4096x4096 computeMatMul, N=1, {tq:.2f} s"}
     out["variants"] = variants
     return out
 
