@@ -88,10 +88,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LK_BENCH_BACKEND=gloo (rehearsal only, never a measurement): the N > 1 code path with
+    # ranks sharing the visible GPUs and gloo collectives, to exercise it on a one-GPU box
+    backend = os.environ.get("LK_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import ggml_hip as G
     G.load_library()
@@ -225,7 +233,8 @@ def main():
         "config": {"workload": "llama7b_token_matmuls_q4_0_n1", "layers": args.layers,
                    "matmuls_per_layer": len(LAYER_MATS), "global_batch": 1, "seq_len": 1,
                    "bytes_per_token": token_bytes,
-                   "parallelism": f"row-shard{world}+rccl-allgather" if world > 1 else "single",
+                   "parallelism": (f"row-shard{world}+{'rccl' if backend == 'nccl' else backend}-allgather" if world > 1
+                                   else "single"),
                    "launches_per_step_per_rank": launches_per_step, "hip_graph": graph is not None,
                    "gpu_ms_per_step": round(ev_ms / args.steps, 4)},
         "roofline": roof,
@@ -276,7 +285,9 @@ def roofline(torch, plans, mats, stream, reps=10):
     avg_s = e0.elapsed_time(e1) / 1e3 / n
     nbytes = sum((r1 - r0) * K // 32 * Q4_0_BLOCK + 4 * K + 4 * (r1 - r0) for (name, M, K, r0, r1) in mats[0])
     achieved = nbytes / avg_s / 1e9
-    traffic, src = pmc_traffic("gemv_stream_kernel<2, 3>")
+    # the committed PMC profile is of the N = 1 layer launch; a row shard is a different launch
+    traffic, src = pmc_traffic("gemv_stream_kernel<2, 3>") if len(mats[0]) and mats[0][0][3] == 0 and \
+        mats[0][0][4] == mats[0][0][1] else (None, None)
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
             "kernel": "gemv_stream_kernel<Q4_0,3> (the 7 matrices of one layer in one launch)",
