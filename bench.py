@@ -250,6 +250,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_batched:
         result["n1_configs"] = n1_configs(torch, G, dev)
         result["batched"] = batched(torch, G, dev)
+        result["next_rows"] = next_rows(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_host_path:
         result["host_path_pcie"] = host_path(torch, G, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -478,6 +479,89 @@ def n1_configs(torch, G, dev, reps=20):
                      "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
                      "rotating_weight_copies": copies, "hip_graph": gr is not None}
         del g
+    return out
+
+
+KQ_BLOCK = {"Q2_K": (84, 80, "f16"), "Q4_K": (144, 0, "f16"), "Q8_K": (292, 0, "f32")}  # bytes, scale offset
+
+
+def _graph_time(torch, fn, s, reps):
+    """Mean seconds per call of `fn` (stream-ordered launches on `s`), graph-replayed."""
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.synchronize()
+    gr = capture(torch, fn, s)
+    run = gr.replay if gr is not None else fn
+    with torch.cuda.stream(s):
+        run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            run()
+        e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / reps, gr is not None
+
+
+def next_rows(torch, G, dev, reps=20):
+    """The SURVEY §8f rows beside the hot path, each at batch 1 on BASELINE shapes, one launch per
+    matrix over rotating copies (> Infinity Cache), graph-replayed, algorithmic GB/s:
+    K-quant dots (Q2_K / Q4_K / Q8_K x F32, kquant_gemv_kernel; synthetic super-blocks: random
+    code bytes, scale fields set to 0.01) and the device dequantizeTensor / quantizeTensor of a
+    Q4_0 11008x4096 matrix (bytes = blocks in + f32 out, or f32 in + blocks out)."""
+    T = G.GGMLType
+    out = {}
+    for name, qn, M, K, copies in (("q2_k_4096x4096_n1", "Q2_K", 4096, 4096, 32),
+                                   ("q4_k_4096x4096_n1", "Q4_K", 4096, 4096, 32),
+                                   ("q8_k_4096x4096_n1", "Q8_K", 4096, 4096, 16),
+                                   ("q4_k_11008x4096_n1", "Q4_K", 11008, 4096, 16)):
+        bb, so, kind = KQ_BLOCK[qn]
+        nblk = M * K // 256
+        nb = nblk * bb
+        g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+        wb, xb, db = g.addBuffer(copies * nb + 256), g.addBuffer(4 * K + 256), g.addBuffer(4 * M * copies + 256)
+        w = g.buffers[wb][: copies * nb].view(copies * nblk, bb)
+        w.copy_(torch.randint(0, 256, w.shape, dtype=torch.uint8, device=dev))
+        if kind == "f16":
+            w[:, so:so + 4].copy_(torch.tensor([0.01, 0.001], dtype=torch.float16).view(torch.uint8).to(dev))
+        else:
+            w[:, so:so + 4].copy_(torch.tensor([0.01], dtype=torch.float32).view(torch.uint8).to(dev))
+        g.buffers[xb][: 4 * K].copy_(torch.randn(K, device=dev).view(torch.uint8))
+        qt = getattr(T, qn)
+        nodes = [(G.GGMLTensor(qt, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [1, K], bufferId=xb),
+                  G.GGMLTensor(T.F32, [1, M], bufferId=db, dataOffset=4 * M * c)) for c in range(copies)]
+        s = torch.cuda.Stream(device=dev)
+
+        def run_all():
+            for (a, b, d) in nodes:
+                G.computeMatMul(g, None, a, b, d, stream=s)
+
+        per, graphed = _graph_time(torch, run_all, s, reps)
+        per /= copies
+        nbytes = nb + 4 * K + 4 * M
+        out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
+                     "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
+                     "kernel": "kquant_gemv_kernel", "rotating_weight_copies": copies, "hip_graph": graphed}
+        del g
+    # format kernels: dequantize / quantize of a Q4_0 11008 x 4096 matrix
+    M, K, copies = 11008, 4096, 8
+    n = M * K
+    nb = n // 32 * BLOCK_BYTES["Q4_0"]
+    g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+    wb = g.addBuffer(copies * nb + 256)
+    src = [torch.randn(n, device=dev) * 0.02 for _ in range(copies)]
+    for c in range(copies):
+        g.buffers[wb][c * nb:(c + 1) * nb].copy_(G.quantizeTensor(src[c], T.Q4_0))
+    ts = [G.GGMLTensor(T.Q4_0, [K, M], bufferId=wb, dataOffset=c * nb) for c in range(copies)]
+    s = torch.cuda.Stream(device=dev)
+    for name, fn, nbytes in (("dequantize_q4_0_11008x4096", lambda: [G.dequantizeTensor(g, t, stream=s) for t in ts], nb + 4 * n),
+                             ("quantize_q4_0_11008x4096", lambda: [G.quantizeTensor(x, T.Q4_0, stream=s) for x in src], 4 * n + nb)):
+        per, graphed = _graph_time(torch, fn, s, reps)
+        per /= copies
+        out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
+                     "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
+                     "rotating_copies": copies, "hip_graph": graphed}
+    del g
     return out
 
 

@@ -693,7 +693,25 @@ int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const
   return LK_OK;
 }
 
-// K-quant x F32: one wave per output (kquant_mul_mat_kernel).
+template <int QT, int NC, bool VX, bool AL>
+void launch_kq_gemv_t(const KQuantArgs &g, hipStream_t st) {
+  dim3 grid((unsigned)((g.M + 3) / 4), (unsigned)((g.N + NC - 1) / NC)), block(256);
+  hipLaunchKernelGGL((kquant_gemv_kernel<QT, NC, VX, AL>), grid, block, 0, st, g);
+}
+
+template <int QT>
+void launch_kq_gemv(const KQuantArgs &g, bool vx, bool al, hipStream_t st) {
+  if (g.N == 1) {
+    if (vx) al ? launch_kq_gemv_t<QT, 1, true, true>(g, st) : launch_kq_gemv_t<QT, 1, true, false>(g, st);
+    else al ? launch_kq_gemv_t<QT, 1, false, true>(g, st) : launch_kq_gemv_t<QT, 1, false, false>(g, st);
+  } else {
+    al ? launch_kq_gemv_t<QT, 4, false, true>(g, st) : launch_kq_gemv_t<QT, 4, false, false>(g, st);
+  }
+}
+
+// K-quant x F32. K % 256 == 0: kquant_gemv_kernel (a wave per row and 1 or 4 columns);
+// otherwise (the Kotlin full-block quirk / flat partial path) kquant_mul_mat_kernel, one wave
+// per output. LK_KQ_LEGACY (set) forces the latter (lab A/B).
 int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   KQuantArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
@@ -701,6 +719,19 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   g.dst = (uint8_t *)dst->data + dst->data_offset;
   g.b_nb0 = b->nb[0]; g.b_nb1 = b->nb[1]; g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
   g.M = c.M; g.N = c.N; g.K = c.K;
+  static const bool legacy = getenv("LK_KQ_LEGACY") != nullptr;  // A/B only
+  if (!legacy && c.K % LK_QK_K == 0 && (c.M + 3) / 4 <= (int64_t)INT32_MAX && (c.N + 3) / 4 <= 65535) {
+    const bool al = ((uintptr_t)g.a & 3) == 0;
+    const bool vx = g.b_nb1 == 4 && ((uintptr_t)g.b & 15) == 0;
+    switch (a->type) {
+      case LK_TYPE_Q2_K: launch_kq_gemv<LK_TYPE_Q2_K>(g, vx, al, st); break;
+      case LK_TYPE_Q4_K: launch_kq_gemv<LK_TYPE_Q4_K>(g, vx, al, st); break;
+      case LK_TYPE_Q8_K: launch_kq_gemv<LK_TYPE_Q8_K>(g, vx, al, st); break;
+      default: return fail(LK_ERR_NOT_IMPLEMENTED, "K-quant: type %d", a->type);
+    }
+    HIP_TRY(hipGetLastError());
+    return LK_OK;
+  }
   const int64_t blocks = (c.M * c.N + 3) / 4;
   if (blocks > (int64_t)INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "output too large for the K-quant kernel");
   dim3 grid((unsigned)blocks), block(256);

@@ -1853,7 +1853,7 @@ struct WideArgs {
 template <int QT>
 __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
   using G = WideGeom<QT>;
-  constexpr int NW = G::NW, MT = G::MT, NT = G::NT, BM = G::BM, BN = G::BN, BB = G::BB, SB = G::SB, D = G::D;
+  constexpr int MT = G::MT, NT = G::NT, BM = G::BM, BN = G::BN, BB = G::BB, SB = G::SB, D = G::D;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2258,6 +2258,141 @@ __global__ __launch_bounds__(256) void kquant_mul_mat_kernel(KQuantArgs g) {
   }
   s = wave_sum(s);
   if (lane == 0) *(float *)(g.dst + j * g.d_nb0 + i * g.d_nb1) = s;
+}
+
+// K % 256 == 0 (every super-block full, row i's blocks are i·K/256 .. +K/256-1): one wave per
+// (row, group of NC columns), the weights of a block decoded once for the NC columns. Lane l
+// owns items 4l .. 4l+3 of every block, which lie in one sub-block, so the scale / min terms are
+// decoded once per block per lane; the quotients q/3, q/15, q/63 come from LDS tables filled
+// with the same correctly rounded division, so every weight is bit-identical to kq_weight
+// (no contraction in this function). U blocks are loaded before any is used. ALIGNED: the
+// block base is 4-byte aligned (BB is a multiple of 4), so header / code bytes load as words.
+template <bool ALIGNED> __device__ __forceinline__ uint32_t kq_ld32(const uint8_t *p) {
+  if constexpr (ALIGNED) return *(const uint32_t *)p;
+  else return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+template <bool ALIGNED> __device__ __forceinline__ uint32_t kq_ld16(const uint8_t *p) {
+  if constexpr (ALIGNED) return *(const uint16_t *)p;
+  else return (uint32_t)p[0] | ((uint32_t)p[1] << 8);
+}
+__device__ __forceinline__ int sext8(uint32_t b) { return (int)(int8_t)(uint8_t)b; }
+
+struct KqTables { float q3[4], q15[16], q63[64]; };
+
+// A lane's raw bytes of one block (loads only; kq_decode turns them into its 4 weights).
+struct KqRaw { uint32_t h, b0, b1, q; };
+
+template <int QT, bool ALIGNED>
+__device__ __forceinline__ KqRaw kq_load(const uint8_t *blk, int lane) {
+  KqRaw r{};
+  if constexpr (QT == LK_TYPE_Q2_K) {  // d | dmin at 80, scale byte l/4, codes byte 16 + l
+    r.h = kq_ld32<ALIGNED>(blk + 80);
+    r.b0 = blk[lane >> 2];
+    r.q = blk[16 + lane];
+  } else if constexpr (QT == LK_TYPE_Q4_K) {  // d | dmin at 0, scale byte 4 + l/8, min-high byte, codes 16 + 2l
+    const int sb = lane >> 3;
+    r.h = kq_ld32<ALIGNED>(blk);
+    r.b0 = blk[4 + sb];
+    r.b1 = blk[4 + min(sb * 2 + 1, LK_K_SCALE_SIZE - 1)];  // masked off in kq_decode past the scales
+    r.q = kq_ld16<ALIGNED>(blk + 4 + LK_K_SCALE_SIZE + 2 * lane);
+  } else {  // Q8_K: f32 d at 0, codes 4 + 4l
+    r.h = kq_ld32<ALIGNED>(blk);
+    r.q = kq_ld32<ALIGNED>(blk + 4 + 4 * lane);
+  }
+  return r;
+}
+
+template <int QT>
+__device__ __forceinline__ void kq_decode(const KqRaw &r, int lane, const KqTables &t, float w[4]) {
+#pragma clang fp contract(off)
+  if constexpr (QT == LK_TYPE_Q2_K) {  // :182-196
+    const float d = h2f(r.h & 0xFFFF), dmin = h2f(r.h >> 16);
+    const int sm = sext8(r.b0);
+    const float scale = t.q15[sm & 0x0F] * d;
+    const float mn = (float)((sm >> 4) & 0x0F) * d + dmin;
+    const int qb = sext8(r.q);
+#pragma unroll
+    for (int e = 0; e < 4; e++) w[e] = t.q3[(qb >> (2 * e)) & 0x03] * scale + mn;
+  } else if constexpr (QT == LK_TYPE_Q4_K) {  // :274-287
+    const float d = h2f(r.h & 0xFFFF), dmin = h2f(r.h >> 16);
+    const int sb = lane >> 3;
+    const int sc = sext8(r.b0);
+    const int qmh = (sb * 2 + 1 < LK_K_SCALE_SIZE) ? (sext8(r.b1) & 0x0F) : 0;
+    const int qm = ((sc >> 6) & 0x03) | (qmh << 2);
+    const float scale = t.q63[sc & 0x3F] * d;
+    const float off = t.q63[qm] * d + dmin;
+#pragma unroll
+    for (int e = 0; e < 4; e++) w[e] = t.q15[(r.q >> (4 * e)) & 0x0F] * scale + off;
+  } else {  // Q8_K :404-407
+    const float d = __builtin_bit_cast(float, r.h);
+#pragma unroll
+    for (int e = 0; e < 4; e++) w[e] = (float)sext8(r.q >> (8 * e)) * d;
+  }
+}
+
+template <int QT, int NC, bool VX, bool ALIGNED>
+__global__ __launch_bounds__(256) void kquant_gemv_kernel(KQuantArgs g) {
+  constexpr int BB = KQTraits<QT>::BB, U = NC == 1 ? 8 : 4;
+  __shared__ KqTables t;
+  {
+    const int x = threadIdx.x;
+    if (x < 64) t.q63[x] = __fdiv_rn((float)x, 63.0f);
+    else if (x < 80) t.q15[x - 64] = __fdiv_rn((float)(x - 64), 15.0f);
+    else if (x < 84) t.q3[x - 80] = __fdiv_rn((float)(x - 80), 3.0f);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (i >= g.M) return;
+  const int64_t j0 = (int64_t)blockIdx.y * NC;
+  const int64_t nb = g.K / LK_QK_K;
+  const uint8_t *row = g.a + i * nb * BB;
+  int64_t jc[NC];  // column of slot c, clamped (loads only; stores are guarded)
+#pragma unroll
+  for (int c = 0; c < NC; c++) jc[c] = min(j0 + c, g.N - 1);
+  float acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; c++) acc[c] = 0.f;
+  for (int64_t s0 = 0; s0 < nb; s0 += U) {
+    // every load of the U blocks first (block index clamped to the row: no guarded loads)
+    KqRaw r[U];
+    float x[U][NC][4];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t sblk = min(s0 + u, nb - 1);
+      r[u] = kq_load<QT, ALIGNED>(row + sblk * BB, lane);
+      const int64_t k = sblk * LK_QK_K + 4 * lane;
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        const uint8_t *xb = g.b + jc[c] * g.b_nb0 + k * g.b_nb1;
+        if constexpr (VX) {
+          const f32x4 xv = *(const f32x4 *)xb;
+          x[u][c][0] = xv.x; x[u][c][1] = xv.y; x[u][c][2] = xv.z; x[u][c][3] = xv.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; e++) x[u][c][e] = *(const float *)(xb + e * g.b_nb1);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      float w[4];
+      kq_decode<QT>(r[u], lane, t, w);
+      const bool live = s0 + u < nb;  // wave-uniform
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        float a = acc[c];
+#pragma unroll
+        for (int e = 0; e < 4; e++) a = fmaf(w[e], x[u][c][e], a);
+        acc[c] = live ? a : acc[c];
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    const float s = wave_sum(acc[c]);
+    if (lane == 0 && (NC == 1 || j0 + c < g.N)) *(float *)(g.dst + (j0 + c) * g.d_nb0 + i * g.d_nb1) = s;
+  }
 }
 
 // ---- format kernels (dequantizeTensor / quantizeTensor) -------------------------

@@ -48,7 +48,9 @@ def test_oracle_block_bound_and_dst_type(qt):
     assert O.compute_mat_mul(a, b, d) == 1
 
 
-GPU_SHAPES = SMALL + [(257, 4096, 1), (64, 11008, 2), (100, 4096, 4)]
+# K % 256 == 0 runs kquant_gemv_kernel (a wave per row, 1 or 4 columns per wave); N = 5, 9 leave
+# a partial column group
+GPU_SHAPES = SMALL + [(257, 4096, 1), (64, 11008, 2), (100, 4096, 4), (33, 2048, 5), (7, 1280, 9)]
 
 
 @pytest.mark.gpu
@@ -66,6 +68,29 @@ def test_kquant_gpu_vs_oracle(gpu, qt, shape):
     got = gpu_matmul(qt, raw, M, K, N, x, host=True, dst_row_pad=2)
     ok, msg = parity_ok(got, ref)
     assert ok, ("host path", msg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("qt", KQ, ids=lambda t: KNAME[t])
+@pytest.mark.parametrize("offs", [(2, 0, 0), (0, 4, 0), (1, 8, 4)], ids=lambda o: "a%d-b%d-d%d" % o)
+def test_kquant_gpu_unaligned_operands(gpu, qt, offs):
+    """Byte-offset weights (the word-load variant needs a 4-aligned block base) and
+    activations off 16 B (no float4 loads) take the byte-load / scalar variants."""
+    from test_gpu_parity import gpu_matmul
+    a_off, b_off, d_off = offs
+    for (M, K, N) in ((19, 1024, 1), (6, 768, 3)):
+        raw = random_kblocks(qt, M * K // 256, seed=M + a_off)
+        x = _x(K, N, 5 + b_off)
+        ref = O.mat_mul_q(qt, raw, M, K, x)
+        got = gpu_matmul(qt, raw, M, K, N, x, a_off=a_off, b_off=b_off, d_off=d_off)
+        ok, msg = parity_ok(got, ref)
+        assert ok, (M, K, N, msg)
+    # a column-strided activation view at N = 1 (k stride != 4)
+    raw = random_kblocks(qt, 4 * 512 // 256, seed=9)
+    x = _x(512, 1, 9)
+    got = gpu_matmul(qt, raw, 4, 512, 1, x, b_stride=3)
+    ok, msg = parity_ok(got, O.mat_mul_q(qt, raw, 4, 512, x))
+    assert ok, msg
 
 
 @pytest.mark.gpu
