@@ -1326,6 +1326,17 @@ int lk_dequantize_device(const lk_tensor *src, float *out, void *stream) {
   if (nblk == 0) return LK_OK;
   hipStream_t st = pick_stream(stream);
   const uint8_t *p = (const uint8_t *)src->data + src->data_offset;
+  static const bool legacy = getenv("LK_FORMAT_LEGACY") != nullptr;  // A/B only
+  if (!legacy && ((uintptr_t)p & 1) == 0 && ((uintptr_t)out & 15) == 0 && (nblk + 31) / 32 <= (int64_t)UINT32_MAX) {
+    dim3 g8((unsigned)((nblk + 31) / 32)), b8(256);  // eight lanes per block
+    switch (src->type) {
+      case LK_TYPE_Q4_0: hipLaunchKernelGGL(dequantize_coop_kernel<LK_TYPE_Q4_0>, g8, b8, 0, st, p, out, nblk); break;
+      case LK_TYPE_Q4_1: hipLaunchKernelGGL(dequantize_coop_kernel<LK_TYPE_Q4_1>, g8, b8, 0, st, p, out, nblk); break;
+      default: hipLaunchKernelGGL(dequantize_coop_kernel<LK_TYPE_Q8_0>, g8, b8, 0, st, p, out, nblk); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return LK_OK;
+  }
   dim3 grid((unsigned)((nblk + 255) / 256)), block(256);
   switch (src->type) {
     case LK_TYPE_Q4_0: hipLaunchKernelGGL(dequantize_kernel<LK_TYPE_Q4_0>, grid, block, 0, st, p, out, nblk); break;
@@ -1343,6 +1354,17 @@ int lk_quantize_device(const float *src, int64_t n, int32_t type, void *out, voi
   if (!src || !out) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
   hipStream_t st = pick_stream(stream);
   const int64_t nblk = n / 32;
+  static const bool legacy = getenv("LK_FORMAT_LEGACY") != nullptr;  // A/B only
+  if (!legacy && ((uintptr_t)src & 15) == 0 && ((uintptr_t)out & 1) == 0 && (nblk + 31) / 32 <= (int64_t)UINT32_MAX) {
+    dim3 g8((unsigned)((nblk + 31) / 32)), b8(256);  // eight lanes per block
+    switch (type) {
+      case LK_TYPE_Q4_0: hipLaunchKernelGGL(quantize_coop_kernel<LK_TYPE_Q4_0>, g8, b8, 0, st, src, (uint8_t *)out, nblk); break;
+      case LK_TYPE_Q4_1: hipLaunchKernelGGL(quantize_coop_kernel<LK_TYPE_Q4_1>, g8, b8, 0, st, src, (uint8_t *)out, nblk); break;
+      default: hipLaunchKernelGGL(quantize_coop_kernel<LK_TYPE_Q8_0>, g8, b8, 0, st, src, (uint8_t *)out, nblk); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return LK_OK;
+  }
   dim3 grid((unsigned)((nblk + 255) / 256)), block(256);
   switch (type) {
     case LK_TYPE_Q4_0: hipLaunchKernelGGL(quantize_kernel<LK_TYPE_Q4_0>, grid, block, 0, st, src, (uint8_t *)out, nblk); break;

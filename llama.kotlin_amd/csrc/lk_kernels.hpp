@@ -2525,6 +2525,109 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float *__restrict__
   }
 }
 
+// quantizeTensor again, eight lanes per block: lane l loads elements 4l..4l+3 (a wave reads 8
+// consecutive blocks = 1 KB contiguous) and writes its code bytes as 16-bit stores (a wave writes
+// its 8 blocks' bytes contiguously); lane 0 of the group writes the f16 header. The block's
+// max / min is a butterfly over the 8 lanes: Kotlin's maxOf / minOf fold (NaN-propagating,
+// -0.0 < +0.0) is associative and commutative, so the tree gives the fold's value. Every other
+// operation is the Kotlin expression with its own rounding (no contraction): bit-identical to
+// quantize_kernel. Needs src 16-byte and out 2-byte aligned (the launcher checks).
+template <int QT>
+__global__ __launch_bounds__(256) void quantize_coop_kernel(const float *__restrict__ src, uint8_t *__restrict__ out, int64_t nblk) {
+#pragma clang fp contract(off)
+  const int64_t gi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t b = min(gi >> 3, nblk - 1);  // tail lanes redo the last block (stores guarded)
+  const bool live = (gi >> 3) < nblk;
+  const int l = threadIdx.x & 7;
+  const f32x4 v = *(const f32x4 *)(src + b * 32 + 4 * l);
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint8_t *o = out + b * QTraits<QT>::BB;
+  auto bfly = [&](float a, bool is_max) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      const float t = __shfl_xor(a, m, 8);
+      a = is_max ? kmax(a, t) : kmin(a, t);
+    }
+    return a;
+  };
+  if constexpr (QT == LK_TYPE_Q8_0 || QT == LK_TYPE_Q4_0) {
+    float amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; e++) amax = kmax(amax, __builtin_fabsf(x[e]));
+    amax = bfly(amax, true);
+    const float scale = (amax == 0.f) ? 1.f : __fdiv_rn(amax, QT == LK_TYPE_Q8_0 ? 127.f : 8.f);
+    const float invS = (QT == LK_TYPE_Q4_0 && scale == 0.f) ? 0.f : __fdiv_rn(1.f, scale);
+    if (!live) return;
+    if (l == 0) *(uint16_t *)o = kotlin_float_to_half(scale);
+    if constexpr (QT == LK_TYPE_Q8_0) {
+      uint32_t q[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++) q[e] = (uint8_t)(int8_t)kround_coerce(x[e] * invS, -128, 127);
+      *(uint16_t *)(o + 2 + 4 * l) = (uint16_t)(q[0] | (q[1] << 8));
+      *(uint16_t *)(o + 4 + 4 * l) = (uint16_t)(q[2] | (q[3] << 8));
+    } else {
+      uint32_t q[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++) q[e] = (uint32_t)kround_coerce(x[e] * invS + 8.f, 0, 15) & 0xF;
+      *(uint16_t *)(o + 2 + 2 * l) = (uint16_t)(q[0] | (q[1] << 4) | (q[2] << 8) | (q[3] << 12));
+    }
+  } else {
+    float fmin = x[0], fmax = x[0];
+#pragma unroll
+    for (int e = 1; e < 4; e++) { fmin = kmin(fmin, x[e]); fmax = kmax(fmax, x[e]); }
+    fmin = bfly(fmin, false);
+    fmax = bfly(fmax, true);
+    float dsc = __fdiv_rn(fmax - fmin, 15.f);
+    if (dsc == 0.f) dsc = 1.f;
+    const float invD = __fdiv_rn(1.f, dsc);
+    if (!live) return;
+    if (l == 0) {
+      *(uint16_t *)o = kotlin_float_to_half(dsc);
+      *(uint16_t *)(o + 2) = kotlin_float_to_half(fmin);
+    }
+    uint32_t q[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) q[e] = (uint32_t)kround_coerce((x[e] - fmin) * invD, 0, 15) & 0xF;
+    *(uint16_t *)(o + 4 + 2 * l) = (uint16_t)(q[0] | (q[1] << 4) | (q[2] << 8) | (q[3] << 12));
+  }
+}
+
+// dequantizeTensor, eight lanes per block: lane l reads its 16-bit code words and writes the 4
+// values 4l..4l+3 as one 16-byte store (a wave writes 1 KB contiguous). Same roundings as
+// dequantize_kernel. Needs blocks 2-byte and out 16-byte aligned (the launcher checks).
+template <int QT>
+__global__ __launch_bounds__(256) void dequantize_coop_kernel(const uint8_t *__restrict__ src, float *__restrict__ out, int64_t nblk) {
+#pragma clang fp contract(off)
+  const int64_t gi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t b = gi >> 3;
+  if (b >= nblk) return;
+  const int l = threadIdx.x & 7;
+  const uint8_t *p = src + b * QTraits<QT>::BB;
+  const float d = h2f(*(const uint16_t *)p);
+  f32x4 r;
+  if constexpr (QT == LK_TYPE_Q8_0) {
+    const uint32_t w = (uint32_t) * (const uint16_t *)(p + 2 + 4 * l) | ((uint32_t) * (const uint16_t *)(p + 4 + 4 * l) << 16);
+    r.x = d * (float)(int8_t)(w & 0xFF);
+    r.y = d * (float)(int8_t)((w >> 8) & 0xFF);
+    r.z = d * (float)(int8_t)((w >> 16) & 0xFF);
+    r.w = d * (float)(int8_t)(w >> 24);
+  } else if constexpr (QT == LK_TYPE_Q4_0) {
+    const uint32_t w = *(const uint16_t *)(p + 2 + 2 * l);
+    r.x = d * ((float)(w & 0xF) - 8.0f);
+    r.y = d * ((float)((w >> 4) & 0xF) - 8.0f);
+    r.z = d * ((float)((w >> 8) & 0xF) - 8.0f);
+    r.w = d * ((float)(w >> 12) - 8.0f);
+  } else {
+    const float m = h2f(*(const uint16_t *)(p + 2));
+    const uint32_t w = *(const uint16_t *)(p + 4 + 2 * l);
+    r.x = d * (float)(w & 0xF) + m;
+    r.y = d * (float)((w >> 4) & 0xF) + m;
+    r.z = d * (float)((w >> 8) & 0xF) + m;
+    r.w = d * (float)(w >> 12) + m;
+  }
+  *(f32x4 *)(out + b * 32 + 4 * l) = r;
+}
+
 // ---- direct dot products (computeDotProduct{F32Q41, F32Q80, Q80Q80, Q40Q40, Q41Q41, Q80Q40},
 // GGMLComputeOps.kt:349-629) ----------------------------------------------------------------
 // One thread per (row, col), k in order, every element / product / sum the Kotlin expression

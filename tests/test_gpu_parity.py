@@ -208,6 +208,11 @@ def test_dequantize_bit_exact(gpu, oracle, qt):
     torch.cuda.synchronize()
     ref = oracle.dequantize(qt, q, n)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    # blocks at an odd byte offset take the one-thread-per-block kernel: same bits
+    t1 = G.GGMLTensor(G.GGMLType(qt), [n], bufferId=ga.addBuffer(q.size + 64), dataOffset=1)
+    ga.setTensorBytes(t1, q)
+    got = G.dequantizeTensor(ga, t1).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
 @pytest.mark.parametrize("qt", Q_TYPES, ids=lambda t: QNAME[t])
@@ -218,10 +223,18 @@ def test_quantize_bit_exact(gpu, oracle, qt):
     parts = [random_weights(32 * 512, 3), random_acts(32 * 512, 4) * np.float32(1e3),
              np.zeros(64, np.float32), np.full(32, 1e-30, np.float32),
              (rng.standard_normal(32 * 64) * np.exp2(rng.uniform(-30, 10, 32 * 64))).astype(np.float32),
-             np.repeat(np.float32([0.5, -0.5, 1.5, 2.5]), 8)]
+             np.repeat(np.float32([0.5, -0.5, 1.5, 2.5]), 8),
+             # NaN / inf / signed zeros: maxOf / minOf propagate NaN and order -0.0 < +0.0, so the
+             # eight-lane butterfly of quantize_coop_kernel must give the sequential fold's value
+             np.float32([np.nan] + [1.0] * 31), np.float32([2.0] * 17 + [np.inf] + [0.5] * 14),
+             np.float32([-0.0, 0.0] * 16), np.float32([0.0] * 31 + [-0.0]), np.float32([-np.inf] + [3.0] * 31)]
     x = np.concatenate(parts).astype(np.float32)
     ref = oracle.quantize(qt, x)
     got = G.quantizeTensor(torch.from_numpy(x).cuda(), G.GGMLType(qt)).cpu().numpy()
+    assert np.array_equal(got, ref)
+    # a source off 16-byte alignment takes the one-thread-per-block kernel: same bytes
+    buf = torch.from_numpy(np.concatenate([np.zeros(1, np.float32), x])).cuda()
+    got = G.quantizeTensor(buf[1:], G.GGMLType(qt)).cpu().numpy()
     assert np.array_equal(got, ref)
 
 
