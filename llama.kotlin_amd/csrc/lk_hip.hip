@@ -723,6 +723,19 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   if (!legacy && c.K % LK_QK_K == 0 && (c.M + 3) / 4 <= (int64_t)INT32_MAX && (c.N + 3) / 4 <= 65535) {
     const bool al = ((uintptr_t)g.a & 3) == 0;
     const bool vx = g.b_nb1 == 4 && ((uintptr_t)g.b & 15) == 0;
+    static const bool no_n1 = getenv("LK_NO_KQ_N1") != nullptr;  // A/B only
+    const size_t xlds = (size_t)(c.K / 32) * 36 * sizeof(float);
+    const uintptr_t need = a->type == LK_TYPE_Q4_K ? 15 : 3;
+    if (!no_n1 && c.N == 1 && ((uintptr_t)g.a & need) == 0 && xlds <= 64 * 1024) {
+      const dim3 grid((unsigned)((c.M + 15) / 16)), block(1024);
+      switch (a->type) {
+        case LK_TYPE_Q2_K: hipLaunchKernelGGL((kquant_n1_kernel<LK_TYPE_Q2_K, 16>), grid, block, xlds, st, g); break;
+        case LK_TYPE_Q4_K: hipLaunchKernelGGL((kquant_n1_kernel<LK_TYPE_Q4_K, 16>), grid, block, xlds, st, g); break;
+        default: hipLaunchKernelGGL((kquant_n1_kernel<LK_TYPE_Q8_K, 16>), grid, block, xlds, st, g); break;
+      }
+      HIP_TRY(hipGetLastError());
+      return LK_OK;
+    }
     switch (a->type) {
       case LK_TYPE_Q2_K: launch_kq_gemv<LK_TYPE_Q2_K>(g, vx, al, st); break;
       case LK_TYPE_Q4_K: launch_kq_gemv<LK_TYPE_Q4_K>(g, vx, al, st); break;

@@ -2395,6 +2395,117 @@ __global__ __launch_bounds__(256) void kquant_gemv_kernel(KQuantArgs g) {
   }
 }
 
+// K-quant x F32 at batch 1 (K % 256 == 0): a lane per 32 consecutive items of a block (lane
+// l of a wave: block l/8 of the chunk, items 32·(l%8) ..), so a wave covers 8 blocks of its row
+// per chunk and a lane's weights are a few wide loads (Q4_K: the 16-byte d / dmin / scales head
+// and the 16 code bytes of its sub-block; Q2_K: d | dmin, its two scale bytes, 8 code bytes;
+// Q8_K: d and 32 code bytes). The activation vector is staged once per workgroup (ROWS rows) in
+// LDS, padded to 36 floats per 32 so a lane's 8 ds_read_b128 spread over the banks. Weights are
+// the Kotlin values bit for bit (kq_weight's formulas, LDS quotient tables, no contraction);
+// only the f32 sum order differs. Chunks go in pairs, loads first. Block bases must be 16-byte
+// (Q4_K) / 4-byte (Q2_K, Q8_K) aligned: the launcher checks.
+__device__ __forceinline__ uint32_t byte_of(const u32x4 &h, int idx) {  // byte idx (0..15), idx wave-varying
+  const uint32_t w = idx < 4 ? h.x : idx < 8 ? h.y : idx < 12 ? h.z : h.w;
+  return (w >> (8 * (idx & 3))) & 0xFF;
+}
+
+template <int QT> struct Kq32Raw;
+template <> struct Kq32Raw<LK_TYPE_Q4_K> { u32x4 h, c; };
+template <> struct Kq32Raw<LK_TYPE_Q2_K> { uint32_t h, sc, c0, c1; };
+template <> struct Kq32Raw<LK_TYPE_Q8_K> { uint32_t d; uint32_t c[8]; };
+
+template <int QT>
+__device__ __forceinline__ Kq32Raw<QT> kq32_load(const uint8_t *blk, int s) {  // s = lane % 8
+  Kq32Raw<QT> r;
+  if constexpr (QT == LK_TYPE_Q4_K) {
+    r.h = *(const u32x4 *)blk;
+    r.c = *(const u32x4 *)(blk + 4 + LK_K_SCALE_SIZE + 16 * s);
+  } else if constexpr (QT == LK_TYPE_Q2_K) {  // sub-blocks 2s, 2s+1: scale bytes 2s, 2s+1; codes 16 + 8s
+    r.h = *(const uint32_t *)(blk + 80);
+    r.sc = *(const uint32_t *)(blk + 4 * (s >> 1)) >> (16 * (s & 1));
+    r.c0 = *(const uint32_t *)(blk + 16 + 8 * s);
+    r.c1 = *(const uint32_t *)(blk + 20 + 8 * s);
+  } else {
+    r.d = *(const uint32_t *)blk;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r.c[j] = *(const uint32_t *)(blk + 4 + 32 * s + 4 * j);
+  }
+  return r;
+}
+
+// a += Σ_e w(item 32s + e) · x[e], e = 0..31 in order
+template <int QT>
+__device__ __forceinline__ float kq32_dot(const Kq32Raw<QT> &r, int s, const KqTables &t, const f32x4 *xv, float a) {
+#pragma clang fp contract(off)
+  float xe[32];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const f32x4 v = xv[j];
+    xe[4 * j] = v.x; xe[4 * j + 1] = v.y; xe[4 * j + 2] = v.z; xe[4 * j + 3] = v.w;
+  }
+  if constexpr (QT == LK_TYPE_Q4_K) {  // :274-287, sub-block s
+    const float d = h2f(r.h.x & 0xFFFF), dmin = h2f(r.h.x >> 16);
+    const int sc = sext8(byte_of(r.h, 4 + s));
+    const int qmh = (s * 2 + 1 < LK_K_SCALE_SIZE) ? (sext8(byte_of(r.h, 5 + 2 * s)) & 0x0F) : 0;
+    const int qm = ((sc >> 6) & 0x03) | (qmh << 2);
+    const float scale = t.q63[sc & 0x3F] * d;
+    const float off = t.q63[qm] * d + dmin;
+    const uint32_t cw[4] = {r.c.x, r.c.y, r.c.z, r.c.w};
+#pragma unroll
+    for (int e = 0; e < 32; e++) a = fmaf(t.q15[(cw[e >> 3] >> (4 * (e & 7))) & 0x0F] * scale + off, xe[e], a);
+  } else if constexpr (QT == LK_TYPE_Q2_K) {  // :182-196, sub-blocks 2s (items 0..15), 2s+1
+    const float d = h2f(r.h & 0xFFFF), dmin = h2f(r.h >> 16);
+#pragma unroll
+    for (int hsb = 0; hsb < 2; hsb++) {
+      const int sm = sext8((r.sc >> (8 * hsb)) & 0xFF);
+      const float scale = t.q15[sm & 0x0F] * d;
+      const float mn = (float)((sm >> 4) & 0x0F) * d + dmin;
+      const uint32_t cw = hsb ? r.c1 : r.c0;  // item 16·hsb + 4m + e: byte m, bits 2e
+#pragma unroll
+      for (int e = 0; e < 16; e++) a = fmaf(t.q3[(cw >> (8 * (e >> 2) + 2 * (e & 3))) & 0x03] * scale + mn, xe[16 * hsb + e], a);
+    }
+  } else {  // Q8_K :404-407
+    const float d = __builtin_bit_cast(float, r.d);
+#pragma unroll
+    for (int e = 0; e < 32; e++) a = fmaf((float)sext8(r.c[e >> 2] >> (8 * (e & 3))) * d, xe[e], a);
+  }
+  return a;
+}
+
+template <int QT, int ROWS>  // rows (waves) per workgroup
+__global__ __launch_bounds__(ROWS * 64) void kquant_n1_kernel(KQuantArgs g) {
+  constexpr int BB = KQTraits<QT>::BB, U = 2;
+  __shared__ KqTables t;
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // (K / 32) x 36 floats
+  const int tid = threadIdx.x;
+  if (tid < 64) t.q63[tid] = __fdiv_rn((float)tid, 63.0f);
+  else if (tid < 80) t.q15[tid - 64] = __fdiv_rn((float)(tid - 64), 15.0f);
+  else if (tid < 84) t.q3[tid - 80] = __fdiv_rn((float)(tid - 80), 3.0f);
+  for (int64_t k = tid; k < g.K; k += ROWS * 64) xs[(k >> 5) * 36 + (k & 31)] = *(const float *)(g.b + k * g.b_nb1);
+  __syncthreads();
+  const int lane = tid & 63;
+  const int64_t i = (int64_t)blockIdx.x * ROWS + __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (i >= g.M) return;
+  const int64_t nb = g.K / LK_QK_K, nch = (nb + 7) / 8;
+  const int s = lane & 7;
+  const uint8_t *row = g.a + i * nb * BB;
+  float acc = 0.f;
+  for (int64_t c0 = 0; c0 < nch; c0 += U) {
+    Kq32Raw<QT> r[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)  // block clamped to the row: never summed when past its end
+      r[u] = kq32_load<QT>(row + min((c0 + u) * 8 + (lane >> 3), nb - 1) * BB, s);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t blk = (c0 + u) * 8 + (lane >> 3);
+      const float a = kq32_dot<QT>(r[u], s, t, (const f32x4 *)(xs + (min(blk, nb - 1) * 8 + s) * 36), acc);
+      acc = blk < nb ? a : acc;
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) *(float *)(g.dst + i * g.d_nb1) = acc;
+}
+
 // ---- format kernels (dequantizeTensor / quantizeTensor) -------------------------
 
 // dequantizeTensor (GGMLComputeOps.kt:918-964): one thread per block, bit-exact

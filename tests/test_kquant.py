@@ -95,6 +95,24 @@ def test_kquant_gpu_unaligned_operands(gpu, qt, offs):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("qt", KQ, ids=lambda t: KNAME[t])
+@pytest.mark.parametrize("K", [1024, 2816])
+def test_kquant_gpu_weights_bit_exact(gpu, qt, K):
+    """One-hot activations turn every output into one weight (x·1 plus exact zeros, any order),
+    so the GPU's decoded weights are compared bit for bit with the oracle's Kotlin-order
+    values: a contraction or a different quotient would show here, not only a tolerance."""
+    from test_gpu_parity import gpu_matmul
+    M = 48
+    raw = random_kblocks(qt, M * K // 256, seed=K + qt)
+    for k in (0, 37, 255, 256 + 129, K - 1):
+        x = np.zeros((K, 1), np.float32)
+        x[k, 0] = 1.0
+        ref = O.mat_mul_q(qt, raw, M, K, x)
+        got = gpu_matmul(qt, raw, M, K, 1, x)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("qt", KQ, ids=lambda t: KNAME[t])
 def test_kquant_gpu_errors_like_oracle(gpu, qt):
     import ggml_hip as G
     raw = np.concatenate([random_kblocks(qt, 2, seed=5), np.zeros(BB[qt], np.uint8)])
