@@ -511,25 +511,26 @@ def next_rows(torch, G, dev, reps=20):
     Q4_0 11008x4096 matrix (bytes = blocks in + f32 out, or f32 in + blocks out)."""
     T = G.GGMLType
     out = {}
-    for name, qn, M, K, copies in (("q2_k_4096x4096_n1", "Q2_K", 4096, 4096, 32),
-                                   ("q4_k_4096x4096_n1", "Q4_K", 4096, 4096, 32),
-                                   ("q8_k_4096x4096_n1", "Q8_K", 4096, 4096, 16),
-                                   ("q4_k_11008x4096_n1", "Q4_K", 11008, 4096, 16)):
+    for name, qn, M, K, N, copies in (("q2_k_4096x4096_n1", "Q2_K", 4096, 4096, 1, 32),
+                                      ("q4_k_4096x4096_n1", "Q4_K", 4096, 4096, 1, 32),
+                                      ("q8_k_4096x4096_n1", "Q8_K", 4096, 4096, 1, 16),
+                                      ("q4_k_11008x4096_n1", "Q4_K", 11008, 4096, 1, 16),
+                                      ("q4_k_11008x4096_n32", "Q4_K", 11008, 4096, 32, 16)):
         bb, so, kind = KQ_BLOCK[qn]
         nblk = M * K // 256
         nb = nblk * bb
         g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
-        wb, xb, db = g.addBuffer(copies * nb + 256), g.addBuffer(4 * K + 256), g.addBuffer(4 * M * copies + 256)
+        wb, xb, db = g.addBuffer(copies * nb + 256), g.addBuffer(4 * K * N + 256), g.addBuffer(4 * M * N * copies + 256)
         w = g.buffers[wb][: copies * nb].view(copies * nblk, bb)
         w.copy_(torch.randint(0, 256, w.shape, dtype=torch.uint8, device=dev))
         if kind == "f16":
             w[:, so:so + 4].copy_(torch.tensor([0.01, 0.001], dtype=torch.float16).view(torch.uint8).to(dev))
         else:
             w[:, so:so + 4].copy_(torch.tensor([0.01], dtype=torch.float32).view(torch.uint8).to(dev))
-        g.buffers[xb][: 4 * K].copy_(torch.randn(K, device=dev).view(torch.uint8))
+        g.buffers[xb][: 4 * K * N].copy_(torch.randn(K * N, device=dev).view(torch.uint8))
         qt = getattr(T, qn)
-        nodes = [(G.GGMLTensor(qt, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [1, K], bufferId=xb),
-                  G.GGMLTensor(T.F32, [1, M], bufferId=db, dataOffset=4 * M * c)) for c in range(copies)]
+        nodes = [(G.GGMLTensor(qt, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [N, K], bufferId=xb),
+                  G.GGMLTensor(T.F32, [N, M], bufferId=db, dataOffset=4 * M * N * c)) for c in range(copies)]
         s = torch.cuda.Stream(device=dev)
 
         def run_all():
@@ -538,10 +539,11 @@ def next_rows(torch, G, dev, reps=20):
 
         per, graphed = _graph_time(torch, run_all, s, reps)
         per /= copies
-        nbytes = nb + 4 * K + 4 * M
+        nbytes = nb + 4 * K * N + 4 * M * N
         out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
                      "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
-                     "kernel": "kquant_gemv_kernel", "rotating_weight_copies": copies, "hip_graph": graphed}
+                     "kernel": "kquant_n1_kernel" if N == 1 else "kquant_gemv_kernel<NC=4>",
+                     "rotating_weight_copies": copies, "hip_graph": graphed}
         del g
     # format kernels: dequantize / quantize of a Q4_0 11008 x 4096 matrix
     M, K, copies = 11008, 4096, 8

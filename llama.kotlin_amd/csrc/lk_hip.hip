@@ -709,6 +709,13 @@ void launch_kq_gemv(const KQuantArgs &g, bool vx, bool al, hipStream_t st) {
   }
 }
 
+template <int QT>
+void launch_kq_nc(int nc, dim3 grid, dim3 block, size_t lds, hipStream_t st, const KQuantArgs &g) {
+  if (nc == 8) hipLaunchKernelGGL((kquant_nc_kernel<QT, 8, 16>), grid, block, lds, st, g);
+  else if (nc == 4) hipLaunchKernelGGL((kquant_nc_kernel<QT, 4, 16>), grid, block, lds, st, g);
+  else hipLaunchKernelGGL((kquant_nc_kernel<QT, 2, 16>), grid, block, lds, st, g);
+}
+
 // K-quant x F32. K % 256 == 0: kquant_gemv_kernel (a wave per row and 1 or 4 columns);
 // otherwise (the Kotlin full-block quirk / flat partial path) kquant_mul_mat_kernel, one wave
 // per output. LK_KQ_LEGACY (set) forces the latter (lab A/B).
@@ -732,6 +739,22 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
         case LK_TYPE_Q2_K: hipLaunchKernelGGL((kquant_n1_kernel<LK_TYPE_Q2_K, 16>), grid, block, xlds, st, g); break;
         case LK_TYPE_Q4_K: hipLaunchKernelGGL((kquant_n1_kernel<LK_TYPE_Q4_K, 16>), grid, block, xlds, st, g); break;
         default: hipLaunchKernelGGL((kquant_n1_kernel<LK_TYPE_Q8_K, 16>), grid, block, xlds, st, g); break;
+      }
+      HIP_TRY(hipGetLastError());
+      return LK_OK;
+    }
+    // batch > 1: NC columns per workgroup staged in LDS (NC = 8 / 4 / 2 as K allows)
+    const size_t col_lds = (size_t)(c.K / 32) * 36 * sizeof(float);
+    int nc = 0;
+    for (int cand : {8, 4, 2})
+      if (nc == 0 && (int64_t)cand <= ((c.N + 1) / 2) * 2 && cand * col_lds <= 150 * 1024) nc = cand;
+    if (!no_n1 && c.N > 1 && nc && ((uintptr_t)g.a & need) == 0 && (c.M + 31) / 32 <= 65535) {
+      const dim3 grid((unsigned)((c.N + nc - 1) / nc), (unsigned)((c.M + 31) / 32)), block(1024);  // 32 rows
+      const size_t lds = nc * col_lds;
+      switch (a->type) {
+        case LK_TYPE_Q2_K: launch_kq_nc<LK_TYPE_Q2_K>(nc, grid, block, lds, st, g); break;
+        case LK_TYPE_Q4_K: launch_kq_nc<LK_TYPE_Q4_K>(nc, grid, block, lds, st, g); break;
+        default: launch_kq_nc<LK_TYPE_Q8_K>(nc, grid, block, lds, st, g); break;
       }
       HIP_TRY(hipGetLastError());
       return LK_OK;

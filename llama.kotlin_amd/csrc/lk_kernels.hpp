@@ -2506,6 +2506,113 @@ __global__ __launch_bounds__(ROWS * 64) void kquant_n1_kernel(KQuantArgs g) {
   if (lane == 0) *(float *)(g.dst + i * g.d_nb1) = acc;
 }
 
+// The weights of a lane's 32 items (kq32_dot's formulas and roundings).
+template <int QT>
+__device__ __forceinline__ void kq32_weights(const Kq32Raw<QT> &r, int s, const KqTables &t, float w[32]) {
+#pragma clang fp contract(off)
+  if constexpr (QT == LK_TYPE_Q4_K) {
+    const float d = h2f(r.h.x & 0xFFFF), dmin = h2f(r.h.x >> 16);
+    const int sc = sext8(byte_of(r.h, 4 + s));
+    const int qmh = (s * 2 + 1 < LK_K_SCALE_SIZE) ? (sext8(byte_of(r.h, 5 + 2 * s)) & 0x0F) : 0;
+    const int qm = ((sc >> 6) & 0x03) | (qmh << 2);
+    const float scale = t.q63[sc & 0x3F] * d;
+    const float off = t.q63[qm] * d + dmin;
+    const uint32_t cw[4] = {r.c.x, r.c.y, r.c.z, r.c.w};
+#pragma unroll
+    for (int e = 0; e < 32; e++) w[e] = t.q15[(cw[e >> 3] >> (4 * (e & 7))) & 0x0F] * scale + off;
+  } else if constexpr (QT == LK_TYPE_Q2_K) {
+    const float d = h2f(r.h & 0xFFFF), dmin = h2f(r.h >> 16);
+#pragma unroll
+    for (int hsb = 0; hsb < 2; hsb++) {
+      const int sm = sext8((r.sc >> (8 * hsb)) & 0xFF);
+      const float scale = t.q15[sm & 0x0F] * d;
+      const float mn = (float)((sm >> 4) & 0x0F) * d + dmin;
+      const uint32_t cw = hsb ? r.c1 : r.c0;
+#pragma unroll
+      for (int e = 0; e < 16; e++) w[16 * hsb + e] = t.q3[(cw >> (8 * (e >> 2) + 2 * (e & 3))) & 0x03] * scale + mn;
+    }
+  } else {
+    const float d = __builtin_bit_cast(float, r.d);
+#pragma unroll
+    for (int e = 0; e < 32; e++) w[e] = (float)sext8(r.c[e >> 2] >> (8 * (e & 3))) * d;
+  }
+}
+
+// K-quant x F32 for batch > 1 (K % 256 == 0): kquant_n1_kernel's lane-per-32-items layout with
+// NC activation columns staged in LDS per workgroup (column-major, the same 36-per-32 padding),
+// each lane's 32 weights decoded once and used for the NC columns. blockIdx.x walks the column
+// groups (so the workgroups sharing a row range run together and its weights hit in L2),
+// blockIdx.y the groups of 32 rows (two rows per wave: each activation read feeds both). The
+// staging reads B(n, k) with n fastest (coalesced for the contiguous [N, K] layout).
+template <int QT, int NC, int ROWS>
+__global__ __launch_bounds__(ROWS * 64) void kquant_nc_kernel(KQuantArgs g) {
+  constexpr int BB = KQTraits<QT>::BB, RPW = 2;  // rows per wave: each x read from LDS feeds both
+  __shared__ KqTables t;
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // NC x (K / 32) x 36 floats
+  const int tid = threadIdx.x;
+  if (tid < 64) t.q63[tid] = __fdiv_rn((float)tid, 63.0f);
+  else if (tid < 80) t.q15[tid - 64] = __fdiv_rn((float)(tid - 64), 15.0f);
+  else if (tid < 84) t.q3[tid - 80] = __fdiv_rn((float)(tid - 80), 3.0f);
+  const int64_t j0 = (int64_t)blockIdx.x * NC;
+  const int64_t XS = (g.K / 32) * 36;
+  for (int64_t idx = tid; idx < g.K * NC; idx += ROWS * 64) {
+    const int c = (int)(idx % NC);
+    const int64_t k = idx / NC;
+    xs[c * XS + (k >> 5) * 36 + (k & 31)] = *(const float *)(g.b + min(j0 + c, g.N - 1) * g.b_nb0 + k * g.b_nb1);
+  }
+  __syncthreads();
+  const int lane = tid & 63;
+  const int64_t i0 = ((int64_t)blockIdx.y * ROWS + __builtin_amdgcn_readfirstlane(tid >> 6)) * RPW;
+  if (i0 >= g.M) return;
+  const int64_t nb = g.K / LK_QK_K, nch = (nb + 7) / 8;
+  const int s = lane & 7;
+  const uint8_t *rows[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; r++) rows[r] = g.a + min(i0 + r, g.M - 1) * nb * BB;  // past M: row M-1, not stored
+  float acc[RPW][NC];
+#pragma unroll
+  for (int r = 0; r < RPW; r++)
+#pragma unroll
+    for (int c = 0; c < NC; c++) acc[r][c] = 0.f;
+  for (int64_t ch = 0; ch < nch; ch++) {
+    const int64_t blk = ch * 8 + (lane >> 3);
+    const int64_t bc = min(blk, nb - 1);  // clamped: never summed when past the row's end
+    Kq32Raw<QT> raw[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; r++) raw[r] = kq32_load<QT>(rows[r] + bc * BB, s);
+    float w[RPW][32];
+#pragma unroll
+    for (int r = 0; r < RPW; r++) kq32_weights<QT>(raw[r], s, t, w[r]);
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      const f32x4 *xv = (const f32x4 *)(xs + c * XS + (bc * 8 + s) * 36);
+      float a[RPW];
+#pragma unroll
+      for (int r = 0; r < RPW; r++) a[r] = acc[r][c];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const f32x4 v = xv[q];
+#pragma unroll
+        for (int r = 0; r < RPW; r++) {
+          a[r] = fmaf(w[r][4 * q], v.x, a[r]);
+          a[r] = fmaf(w[r][4 * q + 1], v.y, a[r]);
+          a[r] = fmaf(w[r][4 * q + 2], v.z, a[r]);
+          a[r] = fmaf(w[r][4 * q + 3], v.w, a[r]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RPW; r++) acc[r][c] = blk < nb ? a[r] : acc[r][c];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; r++)
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      const float sum = wave_sum(acc[r][c]);
+      if (lane == 0 && i0 + r < g.M && j0 + c < g.N) *(float *)(g.dst + (j0 + c) * g.d_nb0 + (i0 + r) * g.d_nb1) = sum;
+    }
+}
+
 // ---- format kernels (dequantizeTensor / quantizeTensor) -------------------------
 
 // dequantizeTensor (GGMLComputeOps.kt:918-964): one thread per block, bit-exact

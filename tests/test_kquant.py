@@ -50,7 +50,8 @@ def test_oracle_block_bound_and_dst_type(qt):
 
 # K % 256 == 0 runs kquant_gemv_kernel (a wave per row, 1 or 4 columns per wave); N = 5, 9 leave
 # a partial column group
-GPU_SHAPES = SMALL + [(257, 4096, 1), (64, 11008, 2), (100, 4096, 4), (33, 2048, 5), (7, 1280, 9)]
+GPU_SHAPES = SMALL + [(257, 4096, 1), (64, 11008, 2), (100, 4096, 4), (33, 2048, 5), (7, 1280, 9),
+                      (40, 4096, 32), (17, 11008, 7)]
 
 
 @pytest.mark.gpu
@@ -109,6 +110,13 @@ def test_kquant_gpu_weights_bit_exact(gpu, qt, K):
         ref = O.mat_mul_q(qt, raw, M, K, x)
         got = gpu_matmul(qt, raw, M, K, 1, x)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+    # batch > 1 (kquant_nc_kernel): column n one-hot at its own k
+    ks = [3, 300, K - 2, 130, 511, 77, K // 2, 1, 1000]
+    x = np.zeros((K, len(ks)), np.float32)
+    x[ks, np.arange(len(ks))] = 1.0
+    ref = O.mat_mul_q(qt, raw, M, K, x)
+    got = gpu_matmul(qt, raw, M, K, len(ks), x)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
 @pytest.mark.gpu
