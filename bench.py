@@ -680,6 +680,26 @@ def host_path(torch, G, dev, layers=LAYERS, reps=5):
                     "h2d_bytes_per_token": int(g.transferBytes(True) * lay),
                     "d2h_bytes_per_token": int(g.transferBytes(False) * lay)}
         g.close()
+    # the plugin path (GGMLHipBackend.graphCompute, core/GGMLCpuBackend.kt:167-176 contract): the
+    # whole token's MUL_MAT graph, cached as one lk_graph; results consumed only by later nodes stay
+    # in HBM, the rest (k, v, gate — read by the CPU ops of a real graph — and the last down) come back
+    dsts = []
+    for a, b, d in nodes:
+        d.op, d.src = G.GGMLOp.MUL_MAT, [a, b]
+        dsts.append(d)
+    be = G.GGMLHipBackend(ga)
+    cg = G.GGMLCGraph(dsts, ga)
+    if be.graphCompute(cg) != G.GGMLStatus.SUCCESS:
+        raise RuntimeError("GGMLHipBackend.graphCompute failed")
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        be.graphCompute(cg)
+    per = (time.perf_counter() - t0) / reps * lay
+    mask = G.backend.writeBackMask(dsts)
+    res["backend"] = {"ms_per_token": round(per * 1e3, 3), "tokens_per_s": round(1 / per, 2),
+                      "d2h_bytes_per_token": int(sum(4 * d.ne[0] * d.ne[1] for d, w in zip(dsts, mask) if w) * lay),
+                      "path": "GGMLHipBackend.graphCompute -> cached lk_graph (ggml_hip/backend.py)"}
+    be.free()
     G.weightsEvictAll()
     return res
 

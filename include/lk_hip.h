@@ -194,8 +194,9 @@ void lk_plan_destroy(lk_plan *plan);
  * GGMLComputeOps.computeGraph / computeMulMat (core/GGMLComputeOps.kt:2515-2652) for a
  * graph of n MUL_MAT nodes on host ByteArrays, kept device-resident between nodes
  * (SURVEY §8f row 2). Nodes are given in graph order; a node that reads bytes an earlier
- * node writes runs after it. Quantized A operands no node writes are weights: pinned once
- * (keyed with weight_generation). Every other range gets a device mirror; a compute
+ * node writes runs after it. Quantized A operands no node writes are weights: pinned at
+ * create with weight_generation (lk_weights_pin semantics); when a later pin of another
+ * generation or an eviction supersedes one, the next compute re-binds to the current mirror. Every other range gets a device mirror; a compute
  * uploads only ranges no earlier node produces, runs each dependency level as one
  * lk_plan, and writes back the dst of nodes with outputs[i] != 0 (outputs = NULL: all).
  * Same results as n lk_mul_mat calls in order. */
@@ -205,6 +206,8 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
 /* Upload inputs, run, write outputs back; synchronous. */
 int lk_graph_compute(lk_graph *g);
 int lk_graph_num_levels(const lk_graph *g);
+/* How many times a compute found a bound weight mirror superseded / evicted and re-bound. */
+int lk_graph_num_rebinds(const lk_graph *g);
 int lk_graph_num_launches(const lk_graph *g);
 /* Bytes one lk_graph_compute moves host->device (to_device = 1) or back (0). */
 uint64_t lk_graph_transfer_bytes(const lk_graph *g, int to_device);
@@ -212,12 +215,28 @@ void lk_graph_destroy(lk_graph *g);
 
 /* ---- weight residency (host path) ------------------------------------------ */
 
-/* Copy a's bytes to a device mirror keyed by (data, data_offset, bytes, generation).
- * A later lk_mul_mat with the same key skips the upload. */
+/* Residency contract (the host ByteArrays stay authoritative, core/GGMLAlloc.kt:271): a
+ * device mirror is current for (ByteArray base, byte range, generation). The caller bumps the
+ * generation whenever it rewrites or re-places bytes a pin covers (GGMLGraphAllocator.
+ * allocateGraph re-placing tensors, core/GGMLAlloc.kt:404-480; reserve replacing a buffer,
+ * :392, :638), or evicts the range. A mirror that is superseded or evicted is never read
+ * again: lk_mul_mat stages the bytes instead, and an lk_graph re-binds its weights at its
+ * next compute.
+ *
+ * lk_weights_pin: make a's bytes current on the device as of `generation`. Same generation
+ * and already covered: nothing is copied. Any current mirror of other generation that
+ * overlaps those bytes is superseded (dropped from the cache; its memory is freed once no
+ * graph holds it). A later lk_mul_mat whose A bytes a current mirror covers skips the upload. */
 int lk_weights_pin(const lk_tensor *a, uint64_t generation);
+/* Drop every current mirror overlapping a's bytes (all devices). */
+int lk_weights_evict(const lk_tensor *a);
+/* Drop every current mirror of the ByteArray at data (buffer replaced or freed). */
+int lk_weights_evict_buffer(const void *data, uint64_t buf_bytes);
+/* Drop every current mirror. Live graphs keep their memory until they re-bind. */
 void lk_weights_evict_all(void);
-/* Bytes currently held by the weight cache. */
+/* Bytes / mirrors currently held by the weight cache (superseded mirrors excluded). */
 uint64_t lk_weights_cached_bytes(void);
+uint64_t lk_weights_cached_count(void);
 /* Pin each row shard of a quantized A on the device lk_mul_mat_sharded(…, n_shards)
  * runs it on (the mirror lk_weights_pin keeps, per shard and device). */
 int lk_weights_pin_sharded(const lk_tensor *a, uint64_t generation, int n_shards);

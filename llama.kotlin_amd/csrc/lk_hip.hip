@@ -14,7 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -56,10 +58,37 @@ namespace {
 // residency cache and staging scratch. lk_mul_mat uses the current device;
 // lk_mul_mat_sharded drives several from one host thread.
 constexpr int kMaxDevices = 64;
+
+// A device mirror of host bytes [lo, lo + bytes) of the ByteArray at `base`, as of weight
+// generation `gen`. Shared: the cache holds one reference while the mirror is current, every
+// lk_graph that bound it holds one, and an lk_mul_mat call holds one while it runs. A pin
+// with another generation over overlapping bytes, lk_weights_evict* and lk_weights_evict_all
+// drop the mirror from the cache and mark it stale; a graph that finds a stale mirror at its
+// next compute re-binds its weights (and rebuilds its plans) from the current cache or the
+// host bytes. The device memory is freed when the last reference goes.
+struct Mirror {
+  int dev = 0;
+  uintptr_t base = 0;
+  uint64_t lo = 0, bytes = 0, gen = 0;
+  void *ptr = nullptr;
+  std::atomic<bool> stale{false};
+  ~Mirror() {
+    if (!ptr) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(dev);
+    (void)hipFree(ptr);  // implicitly synchronizing: in-flight readers finish first
+    (void)hipSetDevice(prev);
+  }
+  bool covers(uintptr_t b, uint64_t l, uint64_t h) const { return b == base && lo <= l && h <= lo + bytes; }
+  bool overlaps(uintptr_t b, uint64_t l, uint64_t h) const { return b == base && l < lo + bytes && lo < h; }
+};
+using MirrorRef = std::shared_ptr<Mirror>;
+
 struct Dev {
   hipStream_t stream = nullptr;
-  // weight residency cache (host path): key = (host base, offset, bytes, generation)
-  std::map<std::tuple<uintptr_t, uint64_t, uint64_t, uint64_t>, void *> weights;
+  // weight residency cache (host path): the current mirrors of this device (guarded by S().cache_mu)
+  std::vector<MirrorRef> weights;
   uint64_t weight_bytes = 0;
   // scratch for the host path: A staging, B, dst span
   void *scratch[3] = {nullptr, nullptr, nullptr};
@@ -67,6 +96,7 @@ struct Dev {
 };
 struct State {
   std::mutex mu;
+  std::mutex cache_mu;  // every Dev::weights / weight_bytes access
   int device = -1;  // the device lk_mul_mat / lk_weights_pin use
   Dev devs[kMaxDevices];
 };
@@ -833,25 +863,67 @@ int init_dev(int d) {
   return LK_OK;
 }
 
-// Device mirror of host bytes [lo, hi) of base if a pinned range covers them.
-const void *find_pinned(Dev &v, const void *base, uint64_t lo, uint64_t hi) {
-  for (auto &kv : v.weights) {
-    auto [b, off, bytes, gen] = kv.first;
-    (void)gen;
-    if (b == (uintptr_t)base && off <= lo && hi <= off + bytes) return (const uint8_t *)kv.second + (lo - off);
-  }
+// The current mirror covering host bytes [lo, hi) of base on this device, or null.
+MirrorRef find_pinned(Dev &v, const void *base, uint64_t lo, uint64_t hi) {
+  std::lock_guard<std::mutex> lk(S().cache_mu);
+  for (auto &m : v.weights)
+    if (m->covers((uintptr_t)base, lo, hi)) return m;
   return nullptr;
 }
 
-int pin_on(Dev &v, const lk_tensor *a, uint64_t lo, uint64_t bytes, uint64_t generation) {
-  auto key = std::make_tuple((uintptr_t)a->data, lo, bytes, generation);
-  if (v.weights.count(key)) return LK_OK;
-  void *dev = nullptr;
-  HIP_TRY(hipMalloc(&dev, std::max<uint64_t>(bytes, 4)));
-  HIP_TRY(hipMemcpy(dev, (const uint8_t *)a->data + lo, bytes, hipMemcpyHostToDevice));
-  v.weights[key] = dev;
+// Drop (and mark stale) every current mirror of `base` on v overlapping [lo, hi) whose
+// generation is not `keep_gen` (all of them when keep_all is false). Caller holds cache_mu.
+int drop_overlapping(Dev &v, uintptr_t base, uint64_t lo, uint64_t hi, bool keep_same_gen, uint64_t keep_gen) {
+  int n = 0;
+  for (size_t i = 0; i < v.weights.size();) {
+    Mirror &m = *v.weights[i];
+    if (m.overlaps(base, lo, hi) && !(keep_same_gen && m.gen == keep_gen)) {
+      m.stale = true;
+      v.weight_bytes -= m.bytes;
+      v.weights.erase(v.weights.begin() + i);
+      n++;
+    } else {
+      i++;
+    }
+  }
+  return n;
+}
+
+// Make host bytes [lo, lo + bytes) of a->data current on device d (the caller made d
+// current) as of `generation`: a current mirror of the same generation covering them is
+// kept; mirrors of other generations overlapping them are superseded (host bytes rewritten).
+int pin_on(int d, const lk_tensor *a, uint64_t lo, uint64_t bytes, uint64_t generation, MirrorRef *out = nullptr) {
+  Dev &v = S().devs[d];
+  const uintptr_t base = (uintptr_t)a->data;
+  std::lock_guard<std::mutex> lk(S().cache_mu);
+  for (auto &m : v.weights)
+    if (m->gen == generation && m->covers(base, lo, lo + bytes)) {
+      if (out) *out = m;
+      return LK_OK;
+    }
+  drop_overlapping(v, base, lo, lo + bytes, true, generation);
+  auto m = std::make_shared<Mirror>();
+  m->dev = d; m->base = base; m->lo = lo; m->bytes = bytes; m->gen = generation;
+  HIP_TRY(hipMalloc(&m->ptr, std::max<uint64_t>(bytes, 4)));
+  HIP_TRY(hipMemcpy(m->ptr, (const uint8_t *)a->data + lo, bytes, hipMemcpyHostToDevice));
+  v.weights.push_back(m);
   v.weight_bytes += bytes;
+  if (out) *out = m;
   return LK_OK;
+}
+
+// Bytes a pin of `a` covers (its whole tensor), as lk_weights_pin computes them.
+uint64_t pin_bytes(const lk_tensor *a) {
+  if (is_q(a->type)) return (uint64_t)(t_num_elements(a) / 32) * block_bytes(a->type);
+  if (is_kq(a->type)) return (uint64_t)(t_num_elements(a) / 256) * kblock_bytes(a->type);
+  return (uint64_t)t_num_elements(a) * (a->type == LK_TYPE_F16 ? 2 : 4);
+}
+
+int evict_range(uintptr_t base, uint64_t lo, uint64_t hi) {
+  std::lock_guard<std::mutex> lk(S().cache_mu);
+  int n = 0;
+  for (auto &v : S().devs) n += drop_overlapping(v, base, lo, hi, false, 0);
+  return n;
 }
 
 }  // namespace
@@ -886,16 +958,42 @@ int lk_init(int device) {
 }
 
 void lk_weights_evict_all(void) {
-  for (auto &v : S().devs) {
-    for (auto &kv : v.weights) (void)hipFree(kv.second);
-    v.weights.clear();
-    v.weight_bytes = 0;
+  std::vector<MirrorRef> gone;  // freed after the lock is released (hipFree synchronizes)
+  {
+    std::lock_guard<std::mutex> lk(S().cache_mu);
+    for (auto &v : S().devs) {
+      for (auto &m : v.weights) { m->stale = true; gone.push_back(m); }
+      v.weights.clear();
+      v.weight_bytes = 0;
+    }
   }
 }
 
+int lk_weights_evict(const lk_tensor *a) {
+  if (!a) return fail(LK_ERR_INVALID_ARG, "evict: null tensor");
+  if (!a->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
+  const uint64_t bytes = pin_bytes(a);
+  evict_range((uintptr_t)a->data, a->data_offset, a->data_offset + std::max<uint64_t>(bytes, 1));
+  return LK_OK;
+}
+
+int lk_weights_evict_buffer(const void *data, uint64_t buf_bytes) {
+  if (!data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
+  evict_range((uintptr_t)data, 0, std::max<uint64_t>(buf_bytes, 1));
+  return LK_OK;
+}
+
 uint64_t lk_weights_cached_bytes(void) {
+  std::lock_guard<std::mutex> lk(S().cache_mu);
   uint64_t t = 0;
   for (auto &v : S().devs) t += v.weight_bytes;
+  return t;
+}
+
+uint64_t lk_weights_cached_count(void) {
+  std::lock_guard<std::mutex> lk(S().cache_mu);
+  uint64_t t = 0;
+  for (auto &v : S().devs) t += v.weights.size();
   return t;
 }
 
@@ -937,17 +1035,14 @@ int lk_weights_pin(const lk_tensor *a, uint64_t generation) {
   int rc = ensure_init();
   if (rc) return rc;
   if (!a || !a->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
-  uint64_t bytes;
-  if (is_q(a->type)) bytes = (uint64_t)(t_num_elements(a) / 32) * block_bytes(a->type);
-  else if (is_kq(a->type)) bytes = (uint64_t)(t_num_elements(a) / 256) * kblock_bytes(a->type);
-  else bytes = (uint64_t)t_num_elements(a) * (a->type == LK_TYPE_F16 ? 2 : 4);
+  const uint64_t bytes = pin_bytes(a);
   if (a->data_offset + bytes > a->buf_bytes) return fail(LK_ERR_OUT_OF_BOUNDS, "pin: tensor exceeds its buffer");
-  return pin_on(cur(), a, a->data_offset, bytes, generation);
+  return pin_on(S().device, a, a->data_offset, bytes, generation);
 }
 
 // Host-buffer operator: the Kotlin drop-in. ByteArrays stay authoritative; A comes
-// from the residency cache when pinned (any generation matching the host range),
-// otherwise it is staged per call.
+// from the residency cache when a current mirror covers its bytes (the latest generation
+// pinned over them: older ones were superseded), otherwise it is staged per call.
 int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   Checked c;
   int rc = check(a, b, dst, &c);
@@ -959,7 +1054,8 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   hipStream_t st = s.stream;
   const uint64_t a_bytes = c.a_hi - c.a_lo, b_bytes = c.b_hi - c.b_lo, d_bytes = c.d_hi - c.d_lo;
   // A: cached mirror or staged copy
-  const void *a_dev = find_pinned(s, a->data, c.a_lo, c.a_hi);
+  const MirrorRef pinned = find_pinned(s, a->data, c.a_lo, c.a_hi);  // held for the call
+  const void *a_dev = pinned ? (const uint8_t *)pinned->ptr + (c.a_lo - pinned->lo) : nullptr;
   if (!a_dev && a_bytes) {
     if ((rc = ensure_scratch(s, 0, a_bytes))) return rc;
     HIP_TRY(hipMemcpyAsync(s.scratch[0], (const uint8_t *)a->data + c.a_lo, a_bytes, hipMemcpyHostToDevice, st));
@@ -1010,6 +1106,7 @@ struct Shard {
   int dev;
   lk_tensor a, d;
   Checked c;
+  MirrorRef pin;  // held for the call
   const void *a_dev;
   uint64_t a_stage_off, d_off;
 };
@@ -1034,7 +1131,7 @@ int lk_weights_pin_sharded(const lk_tensor *a, uint64_t generation, int n_shards
     if (r1 <= r0) continue;
     const int d = r % std::min(ndev, kMaxDevices);
     if ((rc = init_dev(d))) break;
-    rc = pin_on(S().devs[d], a, a->data_offset + (uint64_t)r0 * pitch, (uint64_t)(r1 - r0) * pitch, generation);
+    rc = pin_on(d, a, a->data_offset + (uint64_t)r0 * pitch, (uint64_t)(r1 - r0) * pitch, generation);
   }
   (void)hipSetDevice(prev);
   return rc;
@@ -1079,7 +1176,8 @@ int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, i
     if ((rc = init_dev(x.dev))) goto out;
     Dev &v = S().devs[x.dev];
     used[x.dev] = 1;
-    x.a_dev = find_pinned(v, a->data, x.c.a_lo, x.c.a_hi);
+    x.pin = find_pinned(v, a->data, x.c.a_lo, x.c.a_hi);
+    x.a_dev = x.pin ? (const uint8_t *)x.pin->ptr + (x.c.a_lo - x.pin->lo) : nullptr;
     x.a_stage_off = a_need[x.dev];
     if (!x.a_dev) a_need[x.dev] += (x.c.a_hi - x.c.a_lo + 255) & ~255ull;
     x.d_off = d_need[x.dev];
@@ -1447,11 +1545,22 @@ int lk_repack_q4_device(void *blocks, int64_t n_blocks, int32_t type, int32_t di
 // Intermediate activations never cross PCIe.
 
 struct lk_graph {
-  struct Region { uintptr_t host; uint64_t lo, hi; uint8_t *dev; void *alloc; };
-  struct Copy { uint8_t *host; uint8_t *dev; uint64_t bytes; uint64_t stage; };
+  struct Region { uintptr_t host; uint64_t lo, hi; uint8_t *dev; void *alloc; bool direct; };
+  // direct: the mirror is page-locked host memory the kernels store into (see lk_graph_create);
+  // the copy is then a host memcpy after the sync, no DMA
+  struct Copy { uint8_t *host; uint8_t *dev; uint64_t bytes; uint64_t stage; bool direct; };
   int device = 0;
+  uint64_t generation = 0;
+  int nlev = 0;
   std::vector<Region> regions;
   std::vector<lk_plan *> levels;
+  std::vector<int> plan_level;  // dependency level each plan of `levels` runs
+  // per node: host A descriptor, checks, weight flag, device descriptors, bound weight mirror
+  std::vector<lk_tensor> ha, da, db, dd;
+  std::vector<Checked> c;
+  std::vector<char> a_weight;
+  std::vector<MirrorRef> pins;
+  int rebinds = 0;
   std::vector<Copy> h2d, d2h;
   std::vector<int> node_level;
   uint8_t *staging = nullptr;  // page-locked bounce buffer for the per-compute copies
@@ -1483,6 +1592,62 @@ std::vector<Span> merge_spans(std::vector<Span> v) {
   return out;
 }
 
+// (Re)bind a graph's weights to the current residency cache and build one plan per level.
+// A weight reuses the current mirror covering its bytes (whatever generation a caller
+// pinned last), else it is pinned from the host bytes with the graph's generation. Called at
+// create and again by lk_graph_compute when one of the bound mirrors went stale (superseded
+// or evicted): plans and the captured HIP graph hold raw device pointers, so both are rebuilt.
+int graph_bind(lk_graph *g, bool at_create) {
+  for (auto *p : g->levels) lk_plan_destroy(p);
+  g->levels.clear();
+  g->plan_level.clear();
+  if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  g->exec = nullptr;
+  g->computes = 0;  // first compute after a bind runs eager (sizes scratch), then capture
+  const int n = (int)g->ha.size();
+  int rc = LK_OK;
+  for (int i = 0; i < n; i++) {
+    if (!g->a_weight[i] || g->c[i].empty) continue;
+    const Checked &c = g->c[i];
+    // at create the graph's generation rules (it supersedes other generations over these
+    // bytes); at a rebind whatever a caller pinned since is current
+    MirrorRef m = at_create ? nullptr : find_pinned(S().devs[g->device], g->ha[i].data, c.a_lo, c.a_hi);
+    if (!m && (rc = pin_on(g->device, &g->ha[i], c.a_lo, c.a_hi - c.a_lo, g->generation, &m))) return rc;
+    g->pins[i] = m;
+    g->da[i].data = (uint8_t *)m->ptr + (c.a_lo - m->lo) - c.a_lo;  // base shifted: base + offset = mirror
+    g->da[i].buf_bytes = c.a_hi;
+  }
+  for (int l = 0; l < g->nlev; l++) {
+    std::vector<lk_tensor> la, lb, ld;
+    for (int i = 0; i < n; i++)
+      if (g->node_level[i] == l && !g->c[i].empty) { la.push_back(g->da[i]); lb.push_back(g->db[i]); ld.push_back(g->dd[i]); }
+    if (la.empty()) continue;
+    lk_plan *p = nullptr;
+    if ((rc = lk_plan_create(la.data(), lb.data(), ld.data(), (int)la.size(), &p))) return rc;
+    g->levels.push_back(p);
+    g->plan_level.push_back(l);
+  }
+  return LK_OK;
+}
+
+bool graph_stale(const lk_graph *g) {
+  for (auto &m : g->pins)
+    if (m && m->stale) return true;
+  return false;
+}
+
+// LK_GRAPH_NO_DIRECT=1 (lab A/B): every region in device memory, outputs copied back by DMA
+const bool g_no_direct = [] {
+  const char *e = std::getenv("LK_GRAPH_NO_DIRECT");
+  return e && *e == '1';
+}();
+
+bool direct_at(lk_graph *g, const Span &s) {
+  for (auto &r : g->regions)
+    if (r.host == s.host && r.lo <= s.lo && s.lo < r.hi) return r.direct;
+  return false;
+}
+
 uint8_t *mirror_of(lk_graph *g, uintptr_t host, uint64_t lo) {
   for (auto &r : g->regions)
     if (r.host == host && r.lo <= lo && lo < r.hi) return r.dev + (lo - r.lo);
@@ -1498,7 +1663,8 @@ extern "C" {
 void lk_graph_destroy(lk_graph *g) {
   if (!g) return;
   for (auto *p : g->levels) lk_plan_destroy(p);
-  for (auto &r : g->regions) (void)hipFree(r.alloc);
+  g->pins.clear();
+  for (auto &r : g->regions) (void)(r.direct ? hipHostFree(r.alloc) : hipFree(r.alloc));
   if (g->staging) (void)hipHostFree(g->staging);
   if (g->exec) (void)hipGraphExecDestroy(g->exec);
   delete g;
@@ -1510,7 +1676,6 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
   *out = nullptr;
   int rc = ensure_init();
   if (rc) return rc;
-  Dev &v = cur();
   std::vector<Checked> c(n);
   std::vector<char> a_weight(n, 0);
   std::vector<Span> dsp(n), asp(n), bsp(n);
@@ -1549,17 +1714,6 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
     act.push_back(dsp[i]);
     if (!a_weight[i]) act.push_back(asp[i]);
   }
-  for (auto &s : merge_spans(act)) {
-    // the mirror keeps the host address modulo 256, so operands keep their alignment class
-    lk_graph::Region r{s.host, s.lo, s.hi, nullptr, nullptr};
-    const uint64_t skew = (s.host + s.lo) & 255;
-    if (hipMalloc(&r.alloc, s.hi - s.lo + skew) != hipSuccess) {
-      lk_graph_destroy(g);
-      return fail(LK_ERR_DEVICE, "graph: mirror allocation of %llu B", (unsigned long long)(s.hi - s.lo));
-    }
-    r.dev = (uint8_t *)r.alloc + skew;
-    g->regions.push_back(r);
-  }
   // inputs: read ranges not produced by an earlier node, and non-dense dst ranges (their gap
   // bytes are copied back whole); uploading all of them up front is safe because levels
   // order every in-graph write after the reads that precede it
@@ -1576,13 +1730,41 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
     if (dsp[j].hi - dsp[j].lo != (uint64_t)c[j].M * c[j].N * ew) up.push_back(dsp[j]);
     if (!outputs || outputs[j]) down.push_back(dsp[j]);
   }
+  // A region no node reads, that is not uploaded, holding results the caller wants back (a
+  // graph's pure outputs) is mirrored in page-locked host memory: the kernels store the
+  // results straight over PCIe (a few KB per node) and no DMA copy is queued after them.
+  std::vector<Span> reads;
+  for (int i = 0; i < n; i++) {
+    if (c[i].empty) continue;
+    reads.push_back(bsp[i]);
+    if (!a_weight[i]) reads.push_back(asp[i]);
+  }
+  const std::vector<Span> up_m = merge_spans(up), down_m = merge_spans(down);
+  auto hits = [](const std::vector<Span> &v, const Span &s) {
+    for (auto &x : v) if (overlaps(x, s)) return true;
+    return false;
+  };
+  for (auto &s : merge_spans(act)) {
+    // the mirror keeps the host address modulo 256, so operands keep their alignment class
+    lk_graph::Region r{s.host, s.lo, s.hi, nullptr, nullptr, false};
+    r.direct = !g_no_direct && hits(down_m, s) && !hits(reads, s) && !hits(up_m, s);
+    const uint64_t skew = (s.host + s.lo) & 255;
+    const hipError_t e = r.direct ? hipHostMalloc(&r.alloc, s.hi - s.lo + skew, hipHostMallocDefault)
+                                  : hipMalloc(&r.alloc, s.hi - s.lo + skew);
+    if (e != hipSuccess) {
+      lk_graph_destroy(g);
+      return fail(LK_ERR_DEVICE, "graph: mirror allocation of %llu B", (unsigned long long)(s.hi - s.lo));
+    }
+    r.dev = (uint8_t *)r.alloc + skew;
+    g->regions.push_back(r);
+  }
   // a read range produced by an earlier node is not uploaded even in part: the producer writes it
-  for (auto &s : merge_spans(up)) {
-    g->h2d.push_back({(uint8_t *)s.host + s.lo, mirror_of(g, s.host, s.lo), s.hi - s.lo, 0});
+  for (auto &s : up_m) {
+    g->h2d.push_back({(uint8_t *)s.host + s.lo, mirror_of(g, s.host, s.lo), s.hi - s.lo, 0, false});
     g->h2d_bytes += s.hi - s.lo;
   }
-  for (auto &s : merge_spans(down)) {
-    g->d2h.push_back({(uint8_t *)s.host + s.lo, mirror_of(g, s.host, s.lo), s.hi - s.lo, 0});
+  for (auto &s : down_m) {
+    g->d2h.push_back({(uint8_t *)s.host + s.lo, mirror_of(g, s.host, s.lo), s.hi - s.lo, 0, direct_at(g, s)});
     g->d2h_bytes += s.hi - s.lo;
   }
   // pinned staging for everything that crosses PCIe each compute: the host side of a copy
@@ -1592,41 +1774,33 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
   {
     uint64_t off = 0;
     for (auto &x : g->h2d) { x.stage = off; off += (x.bytes + 255) & ~255ull; }
-    for (auto &x : g->d2h) { x.stage = off; off += (x.bytes + 255) & ~255ull; }
+    for (auto &x : g->d2h) if (!x.direct) { x.stage = off; off += (x.bytes + 255) & ~255ull; }
     if (off && hipHostMalloc((void **)&g->staging, off, hipHostMallocDefault) != hipSuccess) {
       lk_graph_destroy(g);
       return fail(LK_ERR_DEVICE, "graph: pinned staging of %llu B", (unsigned long long)off);
     }
   }
-  // weights, then one plan per level over device descriptors
-  std::vector<lk_tensor> da(n), db(n), dd(n);
+  // device descriptors of the activations; weights and plans are bound by graph_bind
+  g->generation = weight_generation;
+  g->nlev = nlev;
+  g->ha.assign(a, a + n);
+  g->c = c;
+  g->a_weight = a_weight;
+  g->pins.assign(n, nullptr);
+  g->da.resize(n); g->db.resize(n); g->dd.resize(n);
   for (int i = 0; i < n; i++) {
-    da[i] = a[i]; db[i] = b[i]; dd[i] = dst[i];
+    g->da[i] = a[i]; g->db[i] = b[i]; g->dd[i] = dst[i];
     if (c[i].empty) continue;
-    if (a_weight[i]) {
-      const uint64_t bytes = c[i].a_hi - c[i].a_lo;
-      if ((rc = pin_on(v, &a[i], c[i].a_lo, bytes, weight_generation))) { lk_graph_destroy(g); return rc; }
-      const void *p = find_pinned(v, a[i].data, c[i].a_lo, c[i].a_hi);
-      da[i].data = (uint8_t *)p - c[i].a_lo;  // keep data_offset: base shifted so base + offset = mirror
-      da[i].buf_bytes = c[i].a_hi;
-    } else {
-      da[i].data = mirror_of(g, asp[i].host, c[i].a_lo) - c[i].a_lo;
-      da[i].buf_bytes = c[i].a_hi;
+    if (!a_weight[i]) {
+      g->da[i].data = mirror_of(g, asp[i].host, c[i].a_lo) - c[i].a_lo;
+      g->da[i].buf_bytes = c[i].a_hi;
     }
-    db[i].data = mirror_of(g, bsp[i].host, c[i].b_lo) - c[i].b_lo;
-    db[i].buf_bytes = c[i].b_hi;
-    dd[i].data = mirror_of(g, dsp[i].host, c[i].d_lo) - c[i].d_lo;
-    dd[i].buf_bytes = c[i].d_hi;
+    g->db[i].data = mirror_of(g, bsp[i].host, c[i].b_lo) - c[i].b_lo;
+    g->db[i].buf_bytes = c[i].b_hi;
+    g->dd[i].data = mirror_of(g, dsp[i].host, c[i].d_lo) - c[i].d_lo;
+    g->dd[i].buf_bytes = c[i].d_hi;
   }
-  for (int l = 0; l < nlev; l++) {
-    std::vector<lk_tensor> la, lb, ld;
-    for (int i = 0; i < n; i++)
-      if (g->node_level[i] == l && !c[i].empty) { la.push_back(da[i]); lb.push_back(db[i]); ld.push_back(dd[i]); }
-    if (la.empty()) continue;
-    lk_plan *p = nullptr;
-    if ((rc = lk_plan_create(la.data(), lb.data(), ld.data(), (int)la.size(), &p))) { lk_graph_destroy(g); return rc; }
-    g->levels.push_back(p);
-  }
+  if ((rc = graph_bind(g, true))) { lk_graph_destroy(g); return rc; }
   *out = g;
   return LK_OK;
 }
@@ -1635,6 +1809,10 @@ int lk_graph_compute(lk_graph *g) {
   if (!g) return fail(LK_ERR_INVALID_ARG, "null graph");
   int rc = lk_init(g->device);
   if (rc) return rc;
+  if (graph_stale(g)) {  // a bound weight mirror was superseded or evicted since the last bind
+    if ((rc = graph_bind(g, false))) return rc;
+    g->rebinds++;
+  }
   hipStream_t st = cur().stream;
   // device part: staged uploads, every level, staged write-backs — replayed as one HIP graph
   // from the second compute on (the first one sizes any scratch the kernels grow)
@@ -1644,7 +1822,8 @@ int lk_graph_compute(lk_graph *g) {
       int r = lk_plan_launch(p, st);
       if (r) return r;
     }
-    for (auto &x : g->d2h) HIP_TRY(hipMemcpyAsync(g->staging + x.stage, x.dev, x.bytes, hipMemcpyDeviceToHost, st));
+    for (auto &x : g->d2h)
+      if (!x.direct) HIP_TRY(hipMemcpyAsync(g->staging + x.stage, x.dev, x.bytes, hipMemcpyDeviceToHost, st));
     return LK_OK;
   };
   for (auto &x : g->h2d) std::memcpy(g->staging + x.stage, x.host, x.bytes);
@@ -1664,12 +1843,14 @@ int lk_graph_compute(lk_graph *g) {
   if (g->exec) HIP_TRY(hipGraphLaunch(g->exec, st));
   else if ((rc = enqueue())) return rc;
   HIP_TRY(hipStreamSynchronize(st));
-  for (auto &x : g->d2h) std::memcpy(x.host, g->staging + x.stage, x.bytes);
+  for (auto &x : g->d2h) std::memcpy(x.host, x.direct ? x.dev : g->staging + x.stage, x.bytes);
   g->computes++;
   return LK_OK;
 }
 
 int lk_graph_num_levels(const lk_graph *g) { return g ? (int)g->levels.size() : 0; }
+
+int lk_graph_num_rebinds(const lk_graph *g) { return g ? g->rebinds : 0; }
 
 int lk_graph_num_launches(const lk_graph *g) {
   int t = 0;

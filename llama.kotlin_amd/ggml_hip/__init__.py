@@ -19,8 +19,8 @@ from ._lib import (HipDeviceError, IllegalArgumentException, IllegalStateExcepti
 from .backend import GGMLBackendRegistry, GGMLHipBackend, GGMLStatus
 from .ops import (DotKind, MulMatPlan, ResidentGraph, computeDotProductF32Q41, computeDotProductF32Q80, computeDotProductMatrix,
                   computeDotProductQ40Q40, computeDotProductQ41Q41, computeDotProductQ80Q40, computeDotProductQ80Q80, computeMatMul,
-                  computeMatMulSharded, dequantizeTensor, quantizeTensor, to_lk, validateMatMul, weightsEvictAll, weightsPin,
-                  weightsPinSharded)
+                  computeMatMulSharded, dequantizeTensor, quantizeTensor, to_lk, validateMatMul, weightsCachedBytes, weightsCachedCount,
+                  weightsEvict, weightsEvictAll, weightsEvictBuffer, weightsPin, weightsPinSharded)
 from .gguf import GGUFContext, GGUFParser, GGUFTensorInfo, GGUFType, LoadedModel, ModelLoader
 from .sharded import RowShardedMulMat, row_slice, shard_rows
 from .tensor import (GGMLCGraph, GGMLContext, GGMLGraphAllocator, GGMLOp, GGMLTensor, GGMLType,
@@ -30,7 +30,7 @@ __all__ = [
     "GGMLType", "GGMLTensor", "GGMLGraphAllocator", "GGMLContext", "GGMLCGraph", "GGMLOp",
     "calculateContiguousStrides", "calculateTensorByteSize",
     "computeMatMul", "computeMatMulSharded", "weightsPinSharded", "validateMatMul", "MulMatPlan", "ResidentGraph", "dequantizeTensor", "quantizeTensor", "weightsPin",
-    "weightsEvictAll", "to_lk", "DotKind", "computeDotProductMatrix", "computeDotProductF32Q41",
+    "weightsEvictAll", "weightsEvict", "weightsEvictBuffer", "weightsCachedBytes", "weightsCachedCount", "to_lk", "DotKind", "computeDotProductMatrix", "computeDotProductF32Q41",
     "computeDotProductF32Q80", "computeDotProductQ80Q80", "computeDotProductQ40Q40", "computeDotProductQ41Q41",
     "computeDotProductQ80Q40",
     "GGMLHipBackend", "GGMLStatus", "GGMLBackendRegistry",

@@ -77,8 +77,9 @@ EXPORTED_SYMBOLS = (
     "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy", "lk_plan_create_chain",
     "lk_plan_chain_timed_out",
     "lk_graph_create", "lk_graph_compute", "lk_graph_num_levels", "lk_graph_num_launches",
-    "lk_graph_transfer_bytes", "lk_graph_destroy",
-    "lk_weights_pin", "lk_weights_evict_all", "lk_weights_cached_bytes",
+    "lk_graph_transfer_bytes", "lk_graph_destroy", "lk_graph_num_rebinds",
+    "lk_weights_pin", "lk_weights_evict", "lk_weights_evict_buffer", "lk_weights_evict_all",
+    "lk_weights_cached_bytes", "lk_weights_cached_count",
     "lk_dequantize_device", "lk_quantize_device", "lk_dot_direct", "lk_dot_direct_device",
     # include/lk_gguf.h
     "lk_gguf_open_memory", "lk_gguf_open_file", "lk_gguf_close", "lk_gguf_version", "lk_gguf_alignment",
@@ -133,8 +134,12 @@ def load():
     L.lk_graph_destroy.argtypes = [vp]
     L.lk_graph_destroy.restype = None
     L.lk_weights_pin.argtypes = [P, ctypes.c_uint64]
+    L.lk_weights_evict.argtypes = [P]
+    L.lk_weights_evict_buffer.argtypes = [vp, ctypes.c_uint64]
     L.lk_weights_evict_all.restype = None
     L.lk_weights_cached_bytes.restype = ctypes.c_uint64
+    L.lk_weights_cached_count.restype = ctypes.c_uint64
+    L.lk_graph_num_rebinds.argtypes = [vp]
     L.lk_dequantize_device.argtypes = [P, vp, vp]
     L.lk_quantize_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp]
     L.lk_dot_direct.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, vp]

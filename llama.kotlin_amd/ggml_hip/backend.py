@@ -15,6 +15,7 @@ graphCompute catches operator exceptions and returns FAILED exactly as it does t
 from __future__ import annotations
 
 import enum
+from collections import OrderedDict
 
 from . import _lib
 from .ops import MulMatPlan, ResidentGraph, _is_host, computeMatMul
@@ -89,22 +90,57 @@ class GGMLHipBufferType:
         return False
 
 
+def _buffer_table(ga) -> tuple:
+    """(base address, size) of every buffer of the allocator, looked up once per graphCompute."""
+    return tuple((ga.dataPtr(i), ga.bufferSize(i)) if b is not None else (0, 0) for i, b in enumerate(ga.buffers))
+
+
+def _graph_key(ga, nodes, extra) -> tuple:
+    """Everything a plan bakes in about the nodes' tensors — type, shape, strides, offset, buffer
+    (base and size, via the buffer table) — plus `extra` per node, as one flat tuple."""
+    key = [_buffer_table(ga)]
+    for n, e in zip(nodes, extra):
+        for t in (n.src[0], n.src[1], n):
+            key.append(t.type._value_)
+            key.extend(t.ne)
+            key.extend(t.nb)
+            key.append(t.dataOffset)
+            key.append(t.bufferId)
+        key.append(e)
+    return tuple(key)
+
+
+def writeBackMask(nodes) -> list:
+    """Which MUL_MAT results must reach the host ByteArrays: a node flagged as a graph output
+    (GGMLTensor.isOutput, core/GGMLTypes.kt:268) or one no other node of the graph consumes
+    (the caller reads it next: the CPU ops between MUL_MATs in a model graph). Results only
+    consumed by later offloaded nodes stay in HBM."""
+    consumed = {id(s) for n in nodes for s in n.src[:2] if s is not None}
+    return [n.isOutput() or id(n) not in consumed for n in nodes]
+
+
 class GGMLHipBackend:
     """core/GGMLBackend.kt:90-157 implemented on the MI355X.
 
     supportsOp is true exactly for the node types lk_hip computes:
-    MUL_MAT with src0 in {Q4_0, Q4_1, Q8_0} x src1 F32 -> F32, plus the general
+    MUL_MAT with src0 in {Q4_0, Q4_1, Q8_0, Q2_K, Q4_K, Q8_K} x src1 F32 -> F32, plus the general
     F32 x F32 -> F32 and F16 x F16 -> F16 fallbacks. Everything else stays on the CPU
     backend (GGMLBackendManager's AUTO selection, core/GGMLBackendUtils.kt:152-173).
-    """
+
+    Host (ByteArray) allocators: the weights of a graph are mirrored in HBM once per weight
+    generation (include/lk_hip.h residency contract). The caller calls bumpWeightGeneration()
+    whenever the allocator re-places or rewrites tensors (GGMLGraphAllocator.allocateGraph,
+    core/GGMLAlloc.kt:404-480; reserve, :392, :638)."""
 
     GUID = "HIP-GFX950-LLAMAKOTLIN"
+    MAX_CACHED_GRAPHS = 32
 
     def __init__(self, graphAllocator=None, device="cuda"):
         _lib.load()  # fail loudly when the HIP library is absent
         self._bufferType = GGMLHipBufferType(device)
         self.graphAllocator = graphAllocator
-        self._plans: dict = {}
+        self.weightGeneration = 0
+        self._plans: "OrderedDict[tuple, object]" = OrderedDict()
 
     def getGuid(self) -> str:
         return self.GUID
@@ -116,6 +152,13 @@ class GGMLHipBackend:
         for p in self._plans.values():
             p.close()
         self._plans.clear()
+
+    def bumpWeightGeneration(self) -> int:
+        """The host bytes of weights changed: every cached graph re-binds (or is rebuilt) against
+        freshly copied mirrors. Returns the new generation."""
+        self.weightGeneration += 1
+        self.free()
+        return self.weightGeneration
 
     def getDefaultBufferType(self):
         return self._bufferType
@@ -153,12 +196,25 @@ class GGMLHipBackend:
     def offloadOp(self, tensor: GGMLTensor) -> bool:
         return self.supportsOp(tensor)
 
+    def _cached(self, key, make):
+        p = self._plans.get(key)
+        if p is None:
+            p = make()
+            self._plans[key] = p
+            while len(self._plans) > self.MAX_CACHED_GRAPHS:
+                self._plans.popitem(last=False)[1].close()
+        else:
+            self._plans.move_to_end(key)
+        return p
+
     def graphCompute(self, graph: GGMLCGraph) -> GGMLStatus:
         """Compute every MUL_MAT node of the graph (core/GGMLCpuBackend.kt:167-176 contract:
         any operator exception -> FAILED).
 
-        Host (ByteArray) allocators: one ResidentGraph per node set, cached — weights pinned,
-        activations kept in HBM between dependent nodes, levels of independent nodes grouped.
+        Host (ByteArray) allocators: the whole node set is one ResidentGraph (lk_graph), cached
+        by the full tensor descriptors and the weight generation — weights pinned, results that
+        only later nodes consume kept in HBM (writeBackMask), levels of independent nodes grouped
+        into one launch each, the device part replayed as a HIP graph.
         Device allocators: mutually independent nodes run as one plan, otherwise in order."""
         ga = graph.allocator or self.graphAllocator
         try:
@@ -166,24 +222,20 @@ class GGMLHipBackend:
             for n in nodes:
                 if not self.supportsOp(n):
                     raise _lib.NotOffloadedError(f"node {n.name!r} ({n.op}) is not supported by the HIP backend")
-            if nodes and _is_host(ga, nodes[0]):
-                key = ("host",) + tuple((id(n), n.dataOffset, n.src[0].dataOffset, n.src[1].dataOffset,
-                                         ga.dataPtr(n.bufferId), ga.dataPtr(n.src[0].bufferId),
-                                         ga.dataPtr(n.src[1].bufferId)) for n in nodes)
-                g = self._plans.get(key)
-                if g is None:
-                    g = ResidentGraph(ga, [(n.src[0], n.src[1], n) for n in nodes])
-                    self._plans[key] = g
+            if not nodes:
+                return GGMLStatus.SUCCESS
+            if _is_host(ga, nodes[0]):
+                mask = writeBackMask(nodes)
+                key = ("host", self.weightGeneration, id(ga), _graph_key(ga, nodes, mask))
+                g = self._cached(key, lambda: ResidentGraph(ga, [(n.src[0], n.src[1], n) for n in nodes], outputs=mask,
+                                                            weightGeneration=self.weightGeneration))
                 g.compute()
                 return GGMLStatus.SUCCESS
             ids = {id(n) for n in nodes}
             independent = all(id(s) not in ids for n in nodes for s in n.src[:2] if s is not None)
             if independent and len(nodes) > 1:
-                key = tuple((id(n), n.dataOffset, n.src[0].dataOffset, n.src[1].dataOffset) for n in nodes)
-                plan = self._plans.get(key)
-                if plan is None:
-                    plan = MulMatPlan(ga, [(n.src[0], n.src[1], n) for n in nodes])
-                    self._plans[key] = plan
+                key = ("device", id(ga), _graph_key(ga, nodes, [0] * len(nodes)))
+                plan = self._cached(key, lambda: MulMatPlan(ga, [(n.src[0], n.src[1], n) for n in nodes]))
                 plan.launch()
             else:
                 for n in nodes:

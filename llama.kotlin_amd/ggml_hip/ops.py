@@ -60,7 +60,7 @@ class _OnStream:
     stream (handle 0), the launch goes to a library-owned side stream fenced both ways with
     events (side waits for the caller's queue, the caller's queue waits for the launch):
     on the GPU box, launches from this library onto the null stream were observed to be
-    unordered with torch's own null-stream copies (tools/diag3.py: stale dst reads)."""
+    unordered with torch's own null-stream copies (stale dst reads in round 1)."""
 
     def __init__(self, stream=None):
         import torch
@@ -208,6 +208,10 @@ class ResidentGraph:
     def numLaunches(self) -> int:
         return _lib.load().lk_graph_num_launches(self._handle)
 
+    @property
+    def numRebinds(self) -> int:
+        return _lib.load().lk_graph_num_rebinds(self._handle)
+
     def transferBytes(self, toDevice: bool) -> int:
         return int(_lib.load().lk_graph_transfer_bytes(self._handle, 1 if toDevice else 0))
 
@@ -303,8 +307,30 @@ computeDotProductQ80Q40 = _dot_one(DotKind.Q8_0_Q4_0)
 
 
 def weightsPin(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, generation: int = 0):
-    """Host path: keep a device mirror of a's bytes (GGMLBackendBuffer.setTensor residency)."""
+    """Host path: make a device mirror of a's bytes current as of ``generation``
+    (GGMLBackendBuffer.setTensor residency). Pinning the same bytes with another generation
+    supersedes the old mirror (the caller rewrote them); see include/lk_hip.h."""
     _lib.check(_lib.load().lk_weights_pin(ctypes.byref(to_lk(graphAllocator, a)), generation))
+
+
+def weightsEvict(graphAllocator: GGMLGraphAllocator, a: GGMLTensor):
+    """Drop every device mirror overlapping a's bytes."""
+    _lib.check(_lib.load().lk_weights_evict(ctypes.byref(to_lk(graphAllocator, a))))
+
+
+def weightsEvictBuffer(graphAllocator: GGMLGraphAllocator, bufferId: int):
+    """Drop every device mirror of graphAllocator.buffers[bufferId] (the allocator replaced or
+    reset it: core/GGMLAlloc.kt:392, :404-480, :638)."""
+    _lib.check(_lib.load().lk_weights_evict_buffer(ctypes.c_void_p(graphAllocator.dataPtr(bufferId)),
+                                                    graphAllocator.bufferSize(bufferId)))
+
+
+def weightsCachedBytes() -> int:
+    return int(_lib.load().lk_weights_cached_bytes())
+
+
+def weightsCachedCount() -> int:
+    return int(_lib.load().lk_weights_cached_count())
 
 
 def weightsPinSharded(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, nShards: int, generation: int = 0):
@@ -317,4 +343,4 @@ def weightsEvictAll():
 
 
 __all__ = ["computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
-           "weightsEvictAll", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]
+           "weightsEvictAll", "weightsEvict", "weightsEvictBuffer", "weightsCachedBytes", "weightsCachedCount", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]

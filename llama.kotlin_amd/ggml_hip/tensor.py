@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import enum
 import struct
+import weakref
 
 import numpy as np
 
@@ -93,11 +94,14 @@ def calculateContiguousStrides(ne, type_: GGMLType, rank: int | None = None):
     return nb
 
 
+GGML_TENSOR_FLAG_OUTPUT = 1 << 0  # core/GGMLTypes.kt:83
+
+
 class GGMLTensor:
     """core/GGMLTypes.kt:251-270 — a descriptor; bytes live in graphAllocator.buffers[bufferId]."""
 
     def __init__(self, type=GGMLType.F32, ne=None, nb=None, name: str = "", bufferId: int = -1,
-                 dataOffset: int = 0, op: GGMLOp = GGMLOp.NONE, src=None):
+                 dataOffset: int = 0, op: GGMLOp = GGMLOp.NONE, src=None, flags: int = 0):
         self.type = GGMLType(type)
         self.ne = list(ne) if ne is not None else [0] * GGML_MAX_DIMS
         self.ne += [1] * (GGML_MAX_DIMS - len(self.ne)) if len(self.ne) < GGML_MAX_DIMS else []
@@ -107,6 +111,11 @@ class GGMLTensor:
         self.dataOffset = int(dataOffset)
         self.op = op
         self.src = list(src) if src is not None else [None, None]
+        self.flags = int(flags)
+
+    def isOutput(self) -> bool:
+        """core/GGMLTypes.kt:268 (GGML_TENSOR_FLAG_OUTPUT = 1, :83)."""
+        return (self.flags & GGML_TENSOR_FLAG_OUTPUT) != 0
 
     # core/GGMLTypes.kt:275-280
     def rank(self) -> int:
@@ -187,6 +196,12 @@ class GGMLCGraph:
         self.allocator = allocator
 
 
+def _evict_host_buffer(ptr: int, size: int):
+    from . import _lib
+    if _lib._lib is not None:  # nothing can be pinned before the library is loaded
+        _lib._lib.lk_weights_evict_buffer(ptr, size)
+
+
 class GGMLGraphAllocator:
     """core/GGMLAlloc.kt:266-640 — owns the byte buffers tensors point into.
 
@@ -206,7 +221,13 @@ class GGMLGraphAllocator:
 
     def _new_buffer(self, nbytes: int):
         if self.device == "host":
-            return np.zeros(max(nbytes, 0), np.uint8)
+            buf = np.zeros(max(nbytes, 0), np.uint8)
+            # The device weight mirrors are keyed by host address (include/lk_hip.h residency
+            # contract): when this ByteArray goes away its address can come back with other
+            # bytes, so its mirrors are evicted with it.
+            if buf.size:
+                weakref.finalize(buf, _evict_host_buffer, int(buf.ctypes.data), int(buf.size))
+            return buf
         import torch
         return torch.zeros(max(nbytes, 0), dtype=torch.uint8, device=self.device)
 

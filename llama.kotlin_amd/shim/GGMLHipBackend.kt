@@ -2,8 +2,8 @@
 // (src/nativeMain/kotlin/ai/solace/llamakotlin/core/), over the cinterop of include/lk_hip.h.
 //
 // It implements the reference's GGMLBackend plugin interface (K/core/GGMLBackend.kt:90-157)
-// for exactly one op: MUL_MAT with src0 in {Q4_0, Q4_1, Q8_0} (or F32/F16 general) and F32
-// activations, keeping the host ByteArrays authoritative (K/core/GGMLAlloc.kt:271). Every
+// for exactly one op: MUL_MAT with src0 in {Q4_0, Q4_1, Q8_0, Q2_K, Q4_K, Q8_K} (or F32/F16
+// general) and F32 activations, keeping the host ByteArrays authoritative (K/core/GGMLAlloc.kt:271). Every
 // other node is left to GGMLCpuBackend. Not compiled in this repository (no Kotlin/Native
 // toolchain offline); it is the integration contract the C-ABI tests in tests/test_abi.py pin.
 package ai.solace.llamakotlin.core
@@ -52,6 +52,7 @@ private fun fill(t: lk_tensor, src: GGMLTensor, base: CPointer<ByteVar>?, bytes:
  * computeMatMul(graphAllocator, context, a, b, dst) on the MI355X: same signature, same
  * destination-tensor semantics, same exceptions. Weights are mirrored on the device once per
  * (ByteArray, offset, size, generation) by lk_weights_pin; activations and dst are copied per call.
+ * Pass a new weightGeneration after rewriting a weight's bytes in place (include/lk_hip.h).
  */
 fun computeMatMulHip(graphAllocator: GGMLGraphAllocator, @Suppress("unused") context: GGMLContext,
                      a: GGMLTensor, b: GGMLTensor, dst: GGMLTensor, weightGeneration: ULong = 0u,
@@ -118,9 +119,46 @@ fun computeDotProductQ80Q80Hip(graphAllocator: GGMLGraphAllocator, a: GGMLTensor
                                row: Int, col: Int, commonDimK: Int): Float =
     computeDotProductMatrixHip(graphAllocator, LK_DOT_Q8_0_Q8_0, a, b, commonDimK)[row * b.ne[0].toInt() + col]
 
-/** A GGMLBackend that offloads MUL_MAT to the MI355X and defers everything else to the CPU backend. */
+/**
+ * A GGMLBackend that offloads MUL_MAT to the MI355X and defers everything else to the CPU backend.
+ *
+ * graphCompute (K/core/GGMLCpuBackend.kt:167-176 contract) walks the graph in node order
+ * (computeGraph, K/core/GGMLComputeOps.kt:2515-2523) and cuts it into runs of consecutive
+ * offloadable MUL_MAT nodes. Each run is one lk_graph (include/lk_hip.h), created once and cached
+ * by the run's full tensor descriptors and the weight generation: weights stay mirrored in HBM,
+ * independent nodes of a dependency level share one launch, the device part is replayed as a
+ * HIP graph, and only results that leave the run reach the ByteArrays (those flagged isOutput(),
+ * K/core/GGMLTypes.kt:268, read by a node outside the run, or read by no node at all). Nodes the
+ * backend does not offload run one at a time on GGMLCpuBackend between the runs.
+ *
+ * Residency contract: the host ByteArrays stay authoritative. Call bumpWeightGeneration()
+ * whenever GGMLGraphAllocator re-places or rewrites tensor bytes (allocateGraph,
+ * K/core/GGMLAlloc.kt:404-480) and evictBuffer(old) when reserve replaces a buffer (:392, :638).
+ */
 class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) : GGMLBackend {
     private val cpu = GGMLCpuBackend()
+
+    /** The generation cached weight mirrors are current for (lk_weights_pin semantics). */
+    var weightGeneration: ULong = 0u
+        private set
+
+    /** One cached lk_graph: the handle plus the pins that keep its ByteArrays' addresses valid
+     *  (the graph copies inputs from and results to those addresses on every compute). */
+    private class Run(val handle: CPointer<lk_graph>, val pins: List<Pinned<ByteArray>>) {
+        fun close() {
+            lk_graph_destroy(handle)
+            pins.forEach { it.unpin() }
+        }
+    }
+
+    /** Access-ordered LRU of runs, keyed by descriptors + write-back mask + generation. */
+    private val runs = object : LinkedHashMap<List<Long>, Run>(16, 0.75f, true) {
+        override fun removeEldestEntry(eldest: MutableMap.MutableEntry<List<Long>, Run>?): Boolean {
+            if (size <= MAX_CACHED_RUNS) return false
+            eldest?.value?.close()
+            return true
+        }
+    }
 
     init {
         checkStatus(lk_init(device))
@@ -128,8 +166,31 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) :
 
     override fun getGuid(): String = "HIP-GFX950-LK"
     override fun getName(): String = "HIP"
-    override fun free() = lk_shutdown()
+    override fun free() {
+        dropRuns()
+        lk_shutdown()
+    }
     override fun getDefaultBufferType(): GGMLBackendBufferType = cpu.getDefaultBufferType()  // host ByteArrays stay authoritative
+
+    /** The weight bytes changed in place: every cached run is dropped, the next compute pins the
+     *  current bytes under the new generation (superseding the old mirrors). */
+    fun bumpWeightGeneration(): ULong {
+        weightGeneration++
+        dropRuns()
+        return weightGeneration
+    }
+
+    /** A ByteArray the allocator is about to drop or replace: forget its device mirrors. */
+    fun evictBuffer(buffer: ByteArray) {
+        dropRuns()
+        if (buffer.isEmpty()) return
+        buffer.usePinned { checkStatus(lk_weights_evict_buffer(it.addressOf(0), buffer.size.toULong())) }
+    }
+
+    private fun dropRuns() {
+        runs.values.forEach { it.close() }
+        runs.clear()
+    }
 
     override fun supportsOp(tensor: GGMLTensor): Boolean {
         if (tensor.op != GGMLOp.MUL_MAT) return false
@@ -148,20 +209,101 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) :
     override fun graphCompute(graph: GGMLCGraph): GGMLStatus {
         val ga = graph.allocator ?: return GGMLStatus.FAILED
         return try {
-            for (i in 0 until graph.nNodes) {
-                val node = graph.nodes[i] ?: continue
-                if (supportsOp(node)) {
-                    computeMatMulHip(ga, ga.context, node.src[0]!!, node.src[1]!!, node, shards = shards)
-                } else {
+            val nodes = (0 until graph.nNodes).mapNotNull { graph.nodes[it] }
+            var i = 0
+            while (i < nodes.size) {
+                if (!supportsOp(nodes[i])) {
                     // one-node graph on the CPU backend (K/core/GGMLCpuBackend.kt:167-176)
-                    val one = GGMLCGraph(size = 1, nNodes = 1, nodes = arrayOf(node), allocator = ga)
+                    val one = GGMLCGraph(size = 1, nNodes = 1, nodes = arrayOf(nodes[i]), allocator = ga)
                     if (cpu.graphCompute(one) != GGMLStatus.SUCCESS) return GGMLStatus.FAILED
+                    i++
+                    continue
                 }
+                var j = i
+                while (j < nodes.size && supportsOp(nodes[j])) j++
+                if (shards > 1) {
+                    // rows of every MUL_MAT over the node's GPUs: node by node (lk_mul_mat_sharded)
+                    for (k in i until j) {
+                        val n = nodes[k]
+                        computeMatMulHip(ga, ga.context, n.src[0]!!, n.src[1]!!, n, weightGeneration, shards)
+                    }
+                } else {
+                    computeRun(ga, nodes, i, j)
+                }
+                i = j
             }
             GGMLStatus.SUCCESS
         } catch (e: Exception) {
             println("GGMLHipBackend: Error computing graph: ${e.message}")
             GGMLStatus.FAILED
         }
+    }
+
+    /** Nodes [from, to) of `all` (every one offloadable) as one cached lk_graph. */
+    private fun computeRun(ga: GGMLGraphAllocator, all: List<GGMLTensor>, from: Int, to: Int) {
+        val run = all.subList(from, to)
+        val inRun = run.toHashSet()
+        val readBy = HashMap<GGMLTensor, MutableList<GGMLTensor>>()
+        for (n in all) for (s in n.src) if (s != null) readBy.getOrPut(s) { mutableListOf() }.add(n)
+        val writeBack = run.map { n ->
+            val readers = readBy[n].orEmpty()
+            n.isOutput() || readers.isEmpty() || readers.any { it !in inRun }
+        }
+        val bufs = ArrayList<ByteArray?>()
+        fun buf(t: GGMLTensor): ByteArray? = ga.buffers.getOrNull(t.bufferId)
+        val key = ArrayList<Long>(run.size * 3 * 12 + 1)
+        key.add(weightGeneration.toLong())
+        for ((k, n) in run.withIndex()) {
+            for (t in listOf(n.src[0]!!, n.src[1]!!, n)) {
+                val b = buf(t)
+                bufs.add(b)
+                key.add(lkTypeId(t.type).toLong())
+                for (d in 0 until 4) { key.add(t.ne[d]); key.add(t.nb[d].toLong()) }
+                key.add(t.dataOffset.toLong())
+                key.add(b?.let { identityHash(it) } ?: 0L)
+                key.add(b?.size?.toLong() ?: 0L)
+            }
+            key.add(if (writeBack[k]) 1L else 0L)
+        }
+        val cached = runs[key]
+        if (cached != null) {
+            checkStatus(lk_graph_compute(cached.handle))
+            return
+        }
+        // pin every ByteArray the run touches for the graph's lifetime (one Pinned per array)
+        val distinct = bufs.filterNotNull().filter { it.isNotEmpty() }.distinctBy { identityHash(it) }
+        val pins = distinct.map { it.pin() }
+        fun addr(b: ByteArray?): CPointer<ByteVar>? =
+            if (b == null || b.isEmpty()) null else pins.first { it.get() === b }.addressOf(0)
+        val created = memScoped {
+            val n = run.size
+            val la = allocArray<lk_tensor>(n)
+            val lb = allocArray<lk_tensor>(n)
+            val ld = allocArray<lk_tensor>(n)
+            val outs = allocArray<UByteVar>(n)
+            for ((k, node) in run.withIndex()) {
+                val a = node.src[0]!!
+                val b = node.src[1]!!
+                fill(la[k], a, addr(buf(a)), buf(a)?.size ?: 0)
+                fill(lb[k], b, addr(buf(b)), buf(b)?.size ?: 0)
+                fill(ld[k], node, addr(buf(node)), buf(node)?.size ?: 0)
+                outs[k] = if (writeBack[k]) 1u else 0u
+            }
+            val h = alloc<CPointerVar<lk_graph>>()
+            val st = lk_graph_create(la, lb, ld, n, outs, weightGeneration, h.ptr)
+            if (st != LK_OK.toInt()) {
+                pins.forEach { it.unpin() }
+                checkStatus(st)
+            }
+            Run(h.value!!, pins)
+        }
+        runs[key] = created
+        checkStatus(lk_graph_compute(created.handle))
+    }
+
+    private fun identityHash(b: ByteArray): Long = b.usePinned { it.addressOf(0).rawValue.toLong() }
+
+    companion object {
+        const val MAX_CACHED_RUNS = 32
     }
 }

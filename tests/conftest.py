@@ -33,18 +33,3 @@ def gpu():
     ggml_hip.load_library()
     torch.cuda.set_device(0)
     return torch.device("cuda:0")
-
-
-@pytest.fixture(autouse=True)
-def _no_stale_weight_pins(request):
-    """Host weight pins (lk_weights_pin, ResidentGraph) are keyed by host address range, as the
-    Kotlin caller's ByteArrays are, and stay valid until evicted or re-pinned with a new
-    generation. A test's freed numpy buffers can come back at the same addresses in the next
-    test, so every GPU test starts and ends with no pins."""
-    if "gpu" not in request.fixturenames:
-        yield
-        return
-    import ggml_hip as G
-    G.weightsEvictAll()
-    yield
-    G.weightsEvictAll()

@@ -141,8 +141,85 @@ def test_backend_graph_compute_host_uses_resident_graph(gpu, oracle):
     dsts = []
     for a, b, d in nodes:
         d.op, d.src = G.GGMLOp.MUL_MAT, [a, b]
+        d.flags = G.tensor.GGML_TENSOR_FLAG_OUTPUT  # every result wanted on the host
         ga.setTensorBytes(d, np.zeros(4 * d.ne[1], np.uint8))
         dsts.append(d)
     be = G.GGMLHipBackend(ga)
     assert be.graphCompute(G.GGMLCGraph(dsts, ga)) == G.GGMLStatus.SUCCESS
     assert [bytes(ga.tensorBytes(d)) for d in dsts] == want
+
+
+def _mul_mat_nodes(G, nodes):
+    dsts = []
+    for a, b, d in nodes:
+        d.op, d.src = G.GGMLOp.MUL_MAT, [a, b]
+        dsts.append(d)
+    return dsts
+
+
+def test_backend_writes_back_only_what_leaves_the_graph(gpu, oracle):
+    """The backend keeps results that only later MUL_MATs consume in HBM (q -> o, up -> down);
+    every other result (and anything flagged isOutput) reaches the host bytes, equal to the
+    per-node path bit for bit."""
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 20)
+    _, nodes = _layer(ga, oracle)
+    want = _sequential(ga, nodes)
+    dsts = _mul_mat_nodes(G, nodes)
+    assert G.backend.writeBackMask(dsts) == [d.name not in ("q", "u") for d in dsts]
+    dsts[0].flags = G.tensor.GGML_TENSOR_FLAG_OUTPUT  # q is also wanted by the caller
+    for d in dsts:
+        ga.setTensorBytes(d, np.zeros(4 * d.ne[1], np.uint8))
+    be = G.GGMLHipBackend(ga)
+    assert be.graphCompute(G.GGMLCGraph(dsts, ga)) == G.GGMLStatus.SUCCESS
+    for d, w in zip(dsts, want):
+        got = bytes(ga.tensorBytes(d))
+        assert got == (w if d.name != "u" else bytes(len(w))), d.name
+    be.free()
+
+
+def test_backend_cache_keys_on_shapes(gpu):
+    """A graph rebuilt per token at the same offsets with another shape (an F32 MUL_MAT whose
+    K grows, like attention over a growing KV length) must not hit the old plan."""
+    import ggml_hip as G
+    rng = np.random.default_rng(3)
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 16)
+    a_raw = ga.allocateTensor(G.GGMLType.F32, [64, 16])
+    b_raw = ga.allocateTensor(G.GGMLType.F32, [2, 64])
+    d_raw = ga.allocateTensor(G.GGMLType.F32, [2, 16])
+    ga.setTensorBytes(a_raw, rng.standard_normal(64 * 16).astype(np.float32))
+    ga.setTensorBytes(b_raw, rng.standard_normal(2 * 64).astype(np.float32))
+    be = G.GGMLHipBackend(ga)
+    for K in (8, 16, 32, 16):
+        a = G.GGMLTensor(G.GGMLType.F32, [K, 16], bufferId=0, dataOffset=a_raw.dataOffset)
+        b = G.GGMLTensor(G.GGMLType.F32, [2, K], bufferId=0, dataOffset=b_raw.dataOffset)
+        d = G.GGMLTensor(G.GGMLType.F32, [2, 16], bufferId=0, dataOffset=d_raw.dataOffset,
+                         op=G.GGMLOp.MUL_MAT, src=[a, b])
+        assert be.graphCompute(G.GGMLCGraph([d], ga)) == G.GGMLStatus.SUCCESS
+        got = bytes(ga.tensorBytes(d))
+        G.computeMatMul(ga, ga.context, a, b, d)
+        assert got == bytes(ga.tensorBytes(d)), K
+    be.free()
+
+
+def test_backend_weight_generation(gpu, oracle):
+    """The caller rewrites weight bytes and bumps the backend's generation: the next
+    graphCompute reads the new weights."""
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 20)
+    _, nodes = _layer(ga, oracle)
+    dsts = _mul_mat_nodes(G, nodes)
+    be = G.GGMLHipBackend(ga)
+    assert be.graphCompute(G.GGMLCGraph(dsts, ga)) == G.GGMLStatus.SUCCESS
+    a = nodes[0][0]  # wq
+    q = oracle.quantize(2, random_weights(256 * 256, 77))
+    ga.buffers[a.bufferId][a.dataOffset:a.dataOffset + q.size] = q  # in-place, as the Kotlin caller writes
+    be.bumpWeightGeneration()
+    assert be.graphCompute(G.GGMLCGraph(dsts, ga)) == G.GGMLStatus.SUCCESS
+    got = [bytes(ga.tensorBytes(d)) for d in dsts]
+    G.weightsEvictAll()
+    want = _sequential(ga, nodes)
+    for d, g_, w in zip(dsts, got, want):
+        if d.name not in ("q", "u"):
+            assert g_ == w, d.name
+    be.free()
