@@ -617,6 +617,39 @@ def batched(torch, G, dev, reps=10):
                      "mfma_issued_TFLOPs": round(2 * tf, 2), "frac_of_2500TF_bf16": round(2 * tf / 2500, 4),
                      "rotating_weight_copies": copies, "hip_graph": gr is not None}
         del g
+    # C1 on the device: F32 512x512x512 computeMatMul (the general F32 path, A5), timed the same way
+    n, copies = 512, 4
+    g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+    ab = g.addBuffer(4 * n * n * copies + 256)
+    xb = g.addBuffer(4 * n * n + 256)
+    db = g.addBuffer(4 * n * n * copies + 256)
+    g.buffers[ab][: 4 * n * n * copies].copy_(torch.randn(n * n * copies, device=dev).view(torch.uint8))
+    g.buffers[xb][: 4 * n * n].copy_(torch.randn(n * n, device=dev).view(torch.uint8))
+    nodes = [(G.GGMLTensor(T.F32, [n, n], bufferId=ab, dataOffset=4 * n * n * c), G.GGMLTensor(T.F32, [n, n], bufferId=xb),
+              G.GGMLTensor(T.F32, [n, n], bufferId=db, dataOffset=4 * n * n * c)) for c in range(copies)]
+    s = torch.cuda.Stream(device=dev)
+
+    def run_c1():
+        for (a, b, d) in nodes:
+            G.computeMatMul(g, None, a, b, d, stream=s)
+
+    with torch.cuda.stream(s):
+        run_c1()
+    torch.cuda.synchronize()
+    gr = capture(torch, run_c1, s)
+    fn = gr.replay if gr is not None else run_c1
+    with torch.cuda.stream(s):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+    torch.cuda.synchronize()
+    per = e0.elapsed_time(e1) / 1e3 / (reps * copies)
+    out["c1_f32_512x512x512"] = {"avg_launch_us": round(per * 1e6, 3), "GFLOPs": round(2 * n ** 3 / per / 1e9, 1),
+                                 "kernel": "general F32 path (computeMatMul :1530-1543)", "hip_graph": gr is not None}
+    del g
     return out
 
 
@@ -766,8 +799,44 @@ def cpu_baseline(sample_rows, token_bytes, min_seconds=10.0):
     qb = rows * 4096 // 32 * 34 + 4 * 4096 + 4 * rows
     variants["structural_q8_0_4096x4096"] = {"value": round(qb / tq / 1e9, 5), "unit": "GB/s", "cores": 1,
                                              "sample": f"{rows} rows of a Q8_0 4096x4096 computeMatMul, N=1, {tq:.2f} s"}
+    # config C1 (BASELINE configs[0]): F32 512x512x512 computeMatMul on the CPU path, the reference's
+    # own protocol (T/core/GGMLMatMulBenchmarkTest.kt:180-202: 5 warmup runs, 10 timed, mean) on
+    # the shapes/values of T/core/GGMLComputeOpsDestinationTest.kt:218-265 scaled to 512^3
+    # (the benchmark test's F32 generator, :51-56)
+    n = 512
+    a32 = ((np.arange(n * n) + 42) % 127 - 63).astype(np.float32) / np.float32(10.0)
+    b32 = (((np.arange(n * n) + 84) % 127 - 63).astype(np.float32) / np.float32(10.0)).reshape(n, n)
+    for _ in range(5):
+        O.mat_mul_q(O.F32, a32.view(np.uint8), n, n, b32)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        O.mat_mul_q(O.F32, a32.view(np.uint8), n, n, b32)
+    t1 = (time.perf_counter() - t0) / 10
+    variants["c1_f32_512"] = {"value": round(t1 * 1e3, 2), "unit": "ms per computeMatMul", "cores": 1,
+                              "gflops": round(2 * n ** 3 / t1 / 1e9, 4), "higher_is_better": False,
+                              "sample": "structural C restatement, F32 512x512x512, 5 warmup + 10 timed runs, mean"}
     out["variants"] = variants
+    out["host"] = host_cpu()
     return out
+
+
+def host_cpu():
+    """The CPU the baseline ran on (report the GPU box host's model and core count)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 if __name__ == "__main__":

@@ -401,3 +401,22 @@ def test_wide_gemm_vs_oracle(gpu, oracle, qt, shape):
     got = gpu_matmul(qt, q, M, K, N, x, d_off=16, dst_row_pad=5)
     ok, msg = parity_ok(got, ref, noise=noise)
     assert ok, ("strided dst", msg)
+
+
+def test_c1_f32_512_cubed(gpu, oracle):
+    """BASELINE config C1 at its size: F32 512x512x512 through computeMatMul's general path
+    (GGMLComputeOps.kt:1530-1543), the benchmark test's F32 values
+    (T/core/GGMLMatMulBenchmarkTest.kt:51-56, seeds 42 / 84), against the structural oracle."""
+    import ggml_hip as G
+    n = 512
+    a = pattern_f32(n * n, 42)
+    x = pattern_f32(n * n, 84)
+    ref = oracle.mat_mul_q(oracle.F32, a.view(np.uint8), n, n, x.reshape(n, n))
+    ga = G.GGMLGraphAllocator(defaultBufferSize=3 * 4 * n * n + 256)
+    ta = ga.allocateTensor(G.GGMLType.F32, [n, n]); ga.setTensorBytes(ta, a)
+    tb = ga.allocateTensor(G.GGMLType.F32, [n, n]); ga.setTensorBytes(tb, x)
+    td = ga.allocateTensor(G.GGMLType.F32, [n, n])
+    G.computeMatMul(ga, ga.context, ta, tb, td)
+    got = ga.tensorBytes(td).cpu().numpy().view(np.float32).reshape(n, n)
+    ok, msg = parity_ok(got, ref, noise=acc_noise(np.abs(a.reshape(n, n)), np.abs(x.reshape(n, n))))
+    assert ok, msg
