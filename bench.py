@@ -7,15 +7,17 @@ weights (llama.kotlin block layout), F32 activations, F32 outputs — 224 comput
 nodes, 3.65 GB of weights (> the 256 MiB Infinity Cache, so every step streams HBM).
 Weights are random-init N(0, 0.02^2) quantized on device; activations N(0, 1); synthetic.
 
-Schedule of the timed step: the synthetic activations make the 7 matmuls of a layer
-independent nodes, so each layer is one grouped launch (MulMatPlan). The whole step is
-captured once in a HIP graph and replayed (no per-launch host overhead).
-A second line, "decode_chain", times the dependent schedule a real decode has —
-per layer {q,k,v} -> o -> {gate,up} -> down, 4 launches in stream order — on one GPU.
+Schedule of the timed step ("llama7b_token_matmuls_q4_0_n1_layer_grouped"): the 7 matmuls of a
+layer are treated as independent nodes, one grouped launch per layer (MulMatPlan); layer L+1 reads
+layer L's outputs (h <- down, attn <- o, h2 <- v, ffn <- up), so consecutive layers are ordered by
+data. A real decode also orders matrices inside a layer ({q,k,v} -> o -> {gate,up} -> down): that
+schedule is the "decode_chain" line (4 launches per layer), the tokens/s a decoding user sees.
+The whole step is captured once in a HIP graph and replayed (no per-launch host overhead).
 
-Multi-GPU (one process per GPU, RCCL): every weight matrix is row-sharded; after each
-layer rank r all-gathers its rows of the layer's outputs on a separate stream that
-overlaps the next layer. Total work per step is fixed -> "scaling": "strong".
+Multi-GPU (one process per GPU): every weight matrix is row-sharded (rank r owns rows
+[r·M/P, (r+1)·M/P)); each layer is one lk_sharded_plan of the C-ABI — the local rows computed in
+place inside the full output buffers, then one RCCL group of in-place all-gathers over xGMI — and
+the next layer reads the gathered outputs. Total work per step is fixed -> "scaling": "strong".
 
 value = whole-job algorithmic GB/s = Σ_nodes (M·K/32·18 + 4·K + 4·M) bytes per token x
 tokens / wall time (max over ranks). tokens_per_s is reported beside it.
@@ -39,6 +41,8 @@ LAYER_MATS = [("q", HIDDEN, HIDDEN), ("k", HIDDEN, HIDDEN), ("v", HIDDEN, HIDDEN
 # activation each matrix reads: q,k,v share the normed hidden state, gate/up the second one
 X_OF = {"q": "h", "k": "h", "v": "h", "o": "attn", "gate": "h2", "up": "h2", "down": "ffn"}
 X_LEN = {"h": HIDDEN, "attn": HIDDEN, "h2": HIDDEN, "ffn": FFN}
+# layer L+1 reads these outputs of layer L (the timed step's data edge between layers)
+NEXT_X = {"h": "down", "attn": "o", "h2": "v", "ffn": "up"}
 CHAIN = [("q", "k", "v"), ("o",), ("gate", "up"), ("down",)]
 Q4_0_BLOCK = 18
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -106,84 +110,93 @@ def main():
     T = G.GGMLType
 
     # ---- device-resident operands -------------------------------------------------------
+    for (_, M, _) in LAYER_MATS:
+        if M % world:
+            raise SystemExit(f"--gpus {world}: every matrix's rows must split evenly (M = {M})")
     gen = torch.Generator(device=dev)
     gen.manual_seed(0x5EED + rank)
-    mats = []  # per layer: list of (name, M, K, r0, r1)
-    w_bytes = 0
-    for layer in range(args.layers):
-        row = []
-        for (name, M, K) in LAYER_MATS:
-            r0, r1 = shard(M, world, rank)
-            row.append((name, M, K, r0, r1))
-            w_bytes += ((r1 - r0) * K // 32 * Q4_0_BLOCK + 15) // 16 * 16
-        mats.append(row)
-    out_per_layer_padded = sum(-(-M // world) for (_, M, _) in LAYER_MATS)
+    w_bytes = args.layers * sum(((M // world) * K // 32 * Q4_0_BLOCK + 15) // 16 * 16 for (_, M, K) in LAYER_MATS)
+    out_per_layer = sum(M for (_, M, _) in LAYER_MATS)  # every rank holds every layer's FULL outputs
     x_per_layer = sum(X_LEN.values())
     ga = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
-    wbuf = ga.addBuffer(w_bytes + 256)          # all Q4_0 weight shards, back to back
-    xbuf = ga.addBuffer(4 * x_per_layer * args.layers + 256)
-    obuf = ga.addBuffer(4 * out_per_layer_padded * args.layers + 256)
+    wbuf = ga.addBuffer(w_bytes + 256)          # this rank's Q4_0 row shards, back to back
+    xbuf = ga.addBuffer(4 * x_per_layer + 256)   # layer 0's inputs
+    obuf = ga.addBuffer(4 * out_per_layer * args.layers + 256)
+    xs = torch.randn(x_per_layer, generator=gen, device=dev)
+    ga.buffers[xbuf][: 4 * x_per_layer].copy_(xs.view(torch.uint8))
     woff = 0
-    nodes_by_layer = []  # per layer: {name: (a, b, d)}
-    gathered = []
+    nodes_by_layer = []  # per layer: {name: (a_shard, b, dst_full)}
+    local_by_layer = []  # per layer: [(a_shard, b, dst rows of this rank)] — the kernel alone
+    prev = None          # previous layer's {name: dst_full}
     for layer in range(args.layers):
-        xoff, xo = 4 * x_per_layer * layer, {}
-        for key, n in X_LEN.items():
-            xo[key] = xoff
-            xoff += 4 * n
-        xs = torch.randn(x_per_layer, generator=gen, device=dev)
-        base = 4 * x_per_layer * layer
-        ga.buffers[xbuf][base:base + 4 * x_per_layer].copy_(xs.view(torch.uint8))
-        nodes = {}
-        ooff = 4 * out_per_layer_padded * layer
-        for (name, M, K, r0, r1) in mats[layer]:
-            rows = r1 - r0
+        ins, xo = {}, 0
+        for key, n in X_LEN.items():  # layer 0 reads xbuf; layer L+1 reads layer L's outputs
+            ins[key] = (G.GGMLTensor(T.F32, [1, n], bufferId=xbuf, dataOffset=4 * xo) if prev is None
+                        else prev[NEXT_X[key]])
+            xo += n
+        nodes, outs, ooff = {}, {}, 4 * out_per_layer * layer
+        for (name, M, K) in LAYER_MATS:
+            rows = M // world
             a = G.GGMLTensor(T.Q4_0, [K, rows], bufferId=wbuf, dataOffset=woff, name=f"L{layer}.{name}")
             nb = rows * K // 32 * Q4_0_BLOCK
             with torch.no_grad():
                 src = torch.randn(rows * K, generator=gen, device=dev, dtype=torch.float32) * 0.02
-                q = G.quantizeTensor(src, T.Q4_0)
-                ga.buffers[wbuf][woff:woff + nb].copy_(q)
-                del src, q
+                ga.buffers[wbuf][woff:woff + nb].copy_(G.quantizeTensor(src, T.Q4_0))
+                del src
             woff += (nb + 15) // 16 * 16
-            b = G.GGMLTensor(T.F32, [1, K], bufferId=xbuf, dataOffset=xo[X_OF[name]])
-            d = G.GGMLTensor(T.F32, [1, rows], bufferId=obuf, dataOffset=ooff)
-            ooff += 4 * -(-M // world)
-            nodes[name] = (a, b, d)
+            d = G.GGMLTensor(T.F32, [1, M], bufferId=obuf, dataOffset=ooff)
+            ooff += 4 * M
+            nodes[name] = (a, ins[X_OF[name]], d)
+            outs[name] = d
         nodes_by_layer.append(nodes)
-        if world > 1:
-            gathered.append(torch.empty(world * out_per_layer_padded, dtype=torch.float32, device=dev))
-    # timed schedule: per layer one grouped launch of its 7 matrices
-    plans = [[G.MulMatPlan(ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
-    launches_per_step = sum(p.numLaunches for lp in plans for p in lp)
+        local_by_layer.append([(a, b, G.shard_view(d, world, rank)) for (a, b, d) in nodes.values()])
+        prev = outs
+    # timed schedule: per layer one grouped launch of its 7 matrices (independent within the layer);
+    # layer L+1 reads layer L's outputs, so at N > 1 each layer's RCCL all-gather (in the C-ABI,
+    # lk_sharded_plan) sits on the path between consecutive layers
+    comm = None
+    if world > 1 and backend == "nccl":
+        try:
+            comm = G.Comm.from_process_group()
+            plans = [[G.ShardedMulMatPlan(comm, ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
+        except Exception as e:  # noqa: BLE001 — reported in the JSON ("parallelism"), torch's RCCL instead
+            print(f"[bench] lk_comm / lk_sharded_plan failed ({e}); gathering through torch.distributed",
+                  file=sys.stderr)
+            comm = None
+    if comm is not None:
+        pass
+    elif world > 1:  # local launch + torch.distributed gather of the same chunks (gloo rehearsal, or fallback)
+        plans = [[G.MulMatPlan(ga, lp)] for lp in local_by_layer]
+    else:
+        plans = [[G.MulMatPlan(ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
+    local_plans = [[G.MulMatPlan(ga, lp)] for lp in local_by_layer]
+    launches_per_step = sum(p.numLaunches for lp in local_plans for p in lp)
     torch.cuda.synchronize()
 
     compute = torch.cuda.Stream(device=dev)
-    comm = torch.cuda.Stream(device=dev)
-    obuf_f32 = ga.buffers[obuf][: 4 * out_per_layer_padded * args.layers].view(torch.float32)
+    obuf_u8 = ga.buffers[obuf]
+
+    def gloo_gather(layer):
+        # the in-place all-gather of lk_sharded_plan, through torch.distributed (gloo rehearsal / fallback)
+        for (name, M, _) in LAYER_MATS:
+            d = nodes_by_layer[layer][name][2]
+            full = obuf_u8[d.dataOffset:d.dataOffset + 4 * M].view(torch.float32)
+            chunk = M // world
+            parts = list(full.split(chunk))
+            dist.all_gather(parts, parts[rank].clone())
 
     def step():
-        works = []
         for layer, lp in enumerate(plans):
             for plan in lp:
                 plan.launch(stream=compute)
-            if world > 1:
-                ev = torch.cuda.Event()
-                ev.record(compute)
-                comm.wait_event(ev)
-                with torch.cuda.stream(comm):
-                    src = obuf_f32[out_per_layer_padded * layer: out_per_layer_padded * (layer + 1)]
-                    works.append(dist.all_gather_into_tensor(gathered[layer], src, async_op=True))
-        if world > 1:
-            for w in works:
-                w.wait()
-            compute.wait_stream(comm)
+            if world > 1 and comm is None:
+                gloo_gather(layer)
 
     with torch.cuda.stream(compute):
         for _ in range(args.warmup):
             step()
     torch.cuda.synchronize()
-    graph = None if args.no_graph else capture(torch, step, compute)
+    graph = None if (args.no_graph or (world > 1 and backend != "nccl")) else capture(torch, step, compute)
     run = graph.replay if graph is not None else step
     with torch.cuda.stream(compute):
         run()  # one untimed replay (graph upload)
@@ -205,7 +218,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -214,7 +227,7 @@ def main():
     value_gbs = token_bytes * tokens / elapsed / 1e9
     ms_per_step = elapsed * 1e3 / args.steps
 
-    roof = roofline(torch, plans, mats, compute)
+    roof = roofline(torch, local_plans, local_by_layer, compute, world)
 
     result = {
         "metric": "Q4_0 matmul GB/s + tokens/sec 7B, 1/2/4/8 MI355X vs Kotlin CPU",
@@ -230,11 +243,14 @@ def main():
         "vs_baseline": None,
         "dtype": "q4_0 weights x f32 activations, f32 accumulate",
         "data": "synthetic (random-init N(0,0.02^2) weights quantized on device, N(0,1) activations)",
-        "config": {"workload": "llama7b_token_matmuls_q4_0_n1", "layers": args.layers,
+        "config": {"workload": "llama7b_token_matmuls_q4_0_n1_layer_grouped", "layers": args.layers,
                    "matmuls_per_layer": len(LAYER_MATS), "global_batch": 1, "seq_len": 1,
                    "bytes_per_token": token_bytes,
-                   "parallelism": (f"row-shard{world}+{'rccl' if backend == 'nccl' else backend}-allgather" if world > 1
-                                   else "single"),
+                   "schedule": "per layer the 7 matrices as independent nodes in one grouped launch; layer L+1 "
+                               "reads layer L's outputs (at N > 1 after the in-place RCCL all-gather); the "
+                               "intra-layer dependent decode schedule is decode_chain",
+                   "parallelism": (f"row-shard{world}+{'rccl-c-abi' if comm is not None else 'torch-' + backend}-allgather"
+                                   if world > 1 else "single"),
                    "launches_per_step_per_rank": launches_per_step, "hip_graph": graph is not None,
                    "gpu_ms_per_step": round(ev_ms / args.steps, 4)},
         "roofline": roof,
@@ -259,10 +275,15 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
+        for lp in plans:
+            for p in lp:
+                p.close()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 
-def roofline(torch, plans, mats, stream, reps=10):
+def roofline(torch, plans, local_by_layer, stream, world, reps=10):
     """Dominant kernel: the grouped launch of each layer (all 7 matrices, gemv_stream_kernel<Q4_0,3>).
     A HIP graph of the 32 layer launches (distinct weights per layer, so each launch streams HBM)
     is replayed `reps` times between two events on the launch stream; the mean launch duration is
@@ -284,11 +305,10 @@ def roofline(torch, plans, mats, stream, reps=10):
     torch.cuda.synchronize()
     n = reps * len(plans)
     avg_s = e0.elapsed_time(e1) / 1e3 / n
-    nbytes = sum((r1 - r0) * K // 32 * Q4_0_BLOCK + 4 * K + 4 * (r1 - r0) for (name, M, K, r0, r1) in mats[0])
+    nbytes = sum(a.ne[1] * a.ne[0] // 32 * Q4_0_BLOCK + 4 * a.ne[0] + 4 * a.ne[1] for (a, _, _) in local_by_layer[0])
     achieved = nbytes / avg_s / 1e9
     # the committed PMC profile is of the N = 1 layer launch; a row shard is a different launch
-    traffic, src = pmc_traffic("gemv_stream_kernel<2, 3>") if len(mats[0]) and mats[0][0][3] == 0 and \
-        mats[0][0][4] == mats[0][0][1] else (None, None)
+    traffic, src = pmc_traffic("gemv_stream_kernel<2, 3>") if world == 1 else (None, None)
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
             "kernel": "gemv_stream_kernel<Q4_0,3> (the 7 matrices of one layer in one launch)",

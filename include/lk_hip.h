@@ -24,6 +24,8 @@
  *                         MUL_MAT nodes are mutually independent: one launch for the set;
  *                         lk_plan_create_chain: a sequence of dependent stages of such nodes
  *                         (computeGraph's node order, core/GGMLComputeOps.kt:2515) in one launch.
+ *   lk_comm_* / lk_sharded_plan_*  the north star's row sharding over the GPUs of a node with
+ *                         an RCCL all-gather over xGMI (the reference is single-device).
  *   lk_mul_mat_sharded    SURVEY §8b's sharded entry: computeMatMul with A's rows split
  *                         over the GPUs of one node from one host thread (the reference
  *                         is single-device; this is the north star's row sharding).
@@ -189,6 +191,41 @@ int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor
  * then undefined) and re-arms the plan; 0 otherwise. Synchronizes the device. */
 int lk_plan_chain_timed_out(lk_plan *plan);
 void lk_plan_destroy(lk_plan *plan);
+
+/* ---- multi-GPU: row shards + RCCL all-gather over xGMI -----------------
+ * The reference is single-device; this is the north star's partition of the same operator.
+ * Rank r of P owns rows [r·M/P, (r+1)·M/P) of every weight matrix (contiguous bytes: rows are
+ * whole blocks) and computes those rows of dst in place inside the FULL dst; an in-place
+ * ncclAllGather per node fills in the other ranks' rows, so on completion every rank holds
+ * every dst whole — the activations the next MUL_MAT reads.
+ *
+ * One process per GPU: rank 0 calls lk_comm_unique_id, the caller broadcasts the
+ * LK_COMM_ID_BYTES bytes, every rank calls lk_comm_init_rank on its current device.
+ * One process driving several GPUs (the Kotlin host): lk_comm_init_all fills comms[ndev];
+ * launches on different devices go between lk_comm_group_start / lk_comm_group_end. */
+#define LK_COMM_ID_BYTES 128
+typedef struct lk_comm lk_comm;
+int lk_comm_unique_id(void *id);
+int lk_comm_init_rank(const void *id, int nranks, int rank, lk_comm **out);
+int lk_comm_init_all(int ndev, const int *devices, lk_comm **comms);
+int lk_comm_nranks(const lk_comm *comm);
+int lk_comm_rank(const lk_comm *comm);
+void lk_comm_destroy(lk_comm *comm);
+int lk_comm_group_start(void);
+int lk_comm_group_end(void);
+
+/* n independent MUL_MAT nodes, row-sharded over the communicator (device buffers):
+ * a[i] is this rank's row shard (ne[1] = M_i / P), b[i] the full activations, dst[i] the full
+ * destination (ne = [N, M_i], dense rows: nb[1] == N · element size, M_i % P == 0).
+ * lk_sharded_plan_launch enqueues on `stream`: one grouped launch of the local rows, then one
+ * RCCL group of in-place all-gathers. Same bytes in dst as lk_plan_create over the unsharded
+ * nodes (each row is computed by the same kernel from the same bytes). */
+typedef struct lk_sharded_plan lk_sharded_plan;
+int lk_sharded_plan_create(lk_comm *comm, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
+                           lk_sharded_plan **out);
+int lk_sharded_plan_launch(lk_sharded_plan *plan, void *stream);
+int lk_sharded_plan_num_gathers(const lk_sharded_plan *plan);
+void lk_sharded_plan_destroy(lk_sharded_plan *plan);
 
 /* ---- graph residency over host buffers ---------------------------------------
  * GGMLComputeOps.computeGraph / computeMulMat (core/GGMLComputeOps.kt:2515-2652) for a

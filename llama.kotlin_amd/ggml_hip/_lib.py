@@ -80,6 +80,9 @@ EXPORTED_SYMBOLS = (
     "lk_graph_transfer_bytes", "lk_graph_destroy", "lk_graph_num_rebinds",
     "lk_weights_pin", "lk_weights_evict", "lk_weights_evict_buffer", "lk_weights_evict_all",
     "lk_weights_cached_bytes", "lk_weights_cached_count",
+    "lk_comm_unique_id", "lk_comm_init_rank", "lk_comm_init_all", "lk_comm_nranks", "lk_comm_rank",
+    "lk_comm_destroy", "lk_comm_group_start", "lk_comm_group_end",
+    "lk_sharded_plan_create", "lk_sharded_plan_launch", "lk_sharded_plan_num_gathers", "lk_sharded_plan_destroy",
     "lk_dequantize_device", "lk_quantize_device", "lk_dot_direct", "lk_dot_direct_device",
     # include/lk_gguf.h
     "lk_gguf_open_memory", "lk_gguf_open_file", "lk_gguf_close", "lk_gguf_version", "lk_gguf_alignment",
@@ -140,6 +143,18 @@ def load():
     L.lk_weights_cached_bytes.restype = ctypes.c_uint64
     L.lk_weights_cached_count.restype = ctypes.c_uint64
     L.lk_graph_num_rebinds.argtypes = [vp]
+    L.lk_comm_unique_id.argtypes = [vp]
+    L.lk_comm_init_rank.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.lk_comm_init_all.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp)]
+    L.lk_comm_nranks.argtypes = [vp]
+    L.lk_comm_rank.argtypes = [vp]
+    L.lk_comm_destroy.argtypes = [vp]
+    L.lk_comm_destroy.restype = None
+    L.lk_sharded_plan_create.argtypes = [vp, P, P, P, ctypes.c_int, ctypes.POINTER(vp)]
+    L.lk_sharded_plan_launch.argtypes = [vp, vp]
+    L.lk_sharded_plan_num_gathers.argtypes = [vp]
+    L.lk_sharded_plan_destroy.argtypes = [vp]
+    L.lk_sharded_plan_destroy.restype = None
     L.lk_dequantize_device.argtypes = [P, vp, vp]
     L.lk_quantize_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp]
     L.lk_dot_direct.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, vp]

@@ -107,3 +107,114 @@ class RowShardedMulMat:
         else:
             self.gathered.copy_(self.local)
         return self.gathered[: self.spec.M * self.N].view(self.spec.M, self.N)
+
+
+# ---- the C-ABI path: lk_comm (RCCL held by liblk_hip.so) + lk_sharded_plan -----------------
+
+def shard_view(t: GGMLTensor, world: int, rank: int, name: str = "") -> GGMLTensor:
+    """Rows [rank·M/world, (rank+1)·M/world) of a 2-D tensor (A: ne=[K,M]; dst: ne=[N,M]) under the
+    exact split lk_sharded_plan requires (M % world == 0)."""
+    M = t.ne[1]
+    if M % world:
+        raise ValueError(f"M = {M} is not divisible by {world} ranks")
+    per = M // world
+    return row_slice(t, rank * per, (rank + 1) * per, name)
+
+
+class Comm:
+    """An RCCL communicator held by the C-ABI (lk_comm, include/lk_hip.h), on the current device."""
+
+    def __init__(self, handle, nranks: int, rank: int):
+        self._handle = handle
+        self.nranks = nranks
+        self.rank = rank
+
+    @classmethod
+    def from_unique_id(cls, uid: bytes, nranks: int, rank: int) -> "Comm":
+        import ctypes
+        from . import _lib
+        L = _lib.load()
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        _lib.check(L.lk_comm_init_rank(buf, nranks, rank, ctypes.byref(h)))
+        return cls(h, nranks, rank)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+        from . import _lib
+        buf = ctypes.create_string_buffer(128)
+        _lib.check(_lib.load().lk_comm_unique_id(buf))
+        return buf.raw
+
+    @classmethod
+    def single(cls) -> "Comm":
+        """A one-rank communicator (the N = 1 case of the sharded path)."""
+        return cls.from_unique_id(cls.unique_id(), 1, 0)
+
+    @classmethod
+    def from_process_group(cls, group=None) -> "Comm":
+        """Rank 0 makes the id, torch.distributed broadcasts its 128 bytes, every rank joins on its
+        current device (one process per GPU)."""
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        box = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        return cls.from_unique_id(box[0], world, rank)
+
+    def close(self):
+        if self._handle:
+            from . import _lib
+            _lib.load().lk_comm_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ShardedMulMatPlan:
+    """lk_sharded_plan: independent MUL_MAT nodes row-sharded over `comm`. ``nodes`` =
+    [(a_shard, b, dst_full)]: this rank's rows of A (shard_view), the full activations and the
+    FULL destination. One launch computes the local rows in place inside dst_full, then one RCCL
+    group of in-place all-gathers completes every dst_full on every rank."""
+
+    def __init__(self, comm: Comm, ga: GGMLGraphAllocator, nodes):
+        import ctypes
+        from . import _lib
+        from .ops import to_lk
+        L = _lib.load()
+        n = len(nodes)
+        A = (_lib.LkTensor * max(n, 1))()
+        B = (_lib.LkTensor * max(n, 1))()
+        D = (_lib.LkTensor * max(n, 1))()
+        for i, (a, b, d) in enumerate(nodes):
+            A[i], B[i], D[i] = to_lk(ga, a), to_lk(ga, b), to_lk(ga, d)
+        self._handle = ctypes.c_void_p()
+        _lib.check(L.lk_sharded_plan_create(comm._handle, A, B, D, n, ctypes.byref(self._handle)))
+        self.comm = comm
+
+    @property
+    def numGathers(self) -> int:
+        from . import _lib
+        return _lib.load().lk_sharded_plan_num_gathers(self._handle)
+
+    def launch(self, stream=None):
+        from . import _lib
+        from .ops import _OnStream
+        with _OnStream(stream) as sh:
+            _lib.check(_lib.load().lk_sharded_plan_launch(self._handle, sh))
+
+    def close(self):
+        if self._handle:
+            from . import _lib
+            _lib.load().lk_sharded_plan_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

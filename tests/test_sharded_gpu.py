@@ -65,3 +65,53 @@ def test_sharded_errors_and_pins(gpu, oracle):
     assert _lib.load().lk_weights_cached_bytes() == 8 * 2 * 18
     G.weightsEvictAll()
     assert _lib.load().lk_weights_cached_bytes() == 0
+
+
+def test_rccl_sharded_plan_world1_equals_plan(gpu, oracle):
+    """The C-ABI RCCL path (lk_comm + lk_sharded_plan) at world size 1 on the one GPU of the box:
+    bit-equal to lk_plan over the same nodes, and a second plan reading the first one's dst."""
+    import torch
+    import ggml_hip as G
+    from _util import random_acts, random_weights
+    comm = G.Comm.single()
+    assert comm.nranks == 1
+    K, F = 256, 384
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 20)
+    specs = [("q", 2, K, K), ("k", 3, K, K), ("v", 6, K, K), ("gate", 2, K, F), ("up", 2, K, F)]
+    x = ga.allocateTensor(G.GGMLType.F32, [1, K]); ga.setTensorBytes(x, random_acts(K, 1))
+    nodes, ref_nodes = [], []
+    for i, (name, qt, k, m) in enumerate(specs):
+        a = ga.allocateTensor(G.GGMLType(qt), [k, m]); ga.setTensorBytes(a, oracle.quantize(qt, random_weights(k * m, 10 + i)))
+        d = ga.allocateTensor(G.GGMLType.F32, [1, m])
+        dr = ga.allocateTensor(G.GGMLType.F32, [1, m])
+        nodes.append((G.shard_view(a, 1, 0), x, d))
+        ref_nodes.append((a, x, dr))
+    plan = G.ShardedMulMatPlan(comm, ga, nodes)
+    assert plan.numGathers == len(nodes)
+    ref = G.MulMatPlan(ga, ref_nodes)
+    # level 2 reads level 1's (gathered) outputs
+    wd = ga.allocateTensor(G.GGMLType.Q4_0, [F, K]); ga.setTensorBytes(wd, oracle.quantize(2, random_weights(F * K, 99)))
+    d2 = ga.allocateTensor(G.GGMLType.F32, [1, K])
+    d2r = ga.allocateTensor(G.GGMLType.F32, [1, K])
+    plan2 = G.ShardedMulMatPlan(comm, ga, [(G.shard_view(wd, 1, 0), nodes[4][2], d2)])
+    ref2 = G.MulMatPlan(ga, [(wd, ref_nodes[4][2], d2r)])
+    s = torch.cuda.Stream()
+    for _ in range(2):
+        plan.launch(stream=s); plan2.launch(stream=s)
+        ref.launch(stream=s); ref2.launch(stream=s)
+    torch.cuda.synchronize()
+    for (_, _, d), (_, _, dr) in zip(nodes + [(None, None, d2)], ref_nodes + [(None, None, d2r)]):
+        assert bytes(ga.tensorBytes(d).cpu().numpy()) == bytes(ga.tensorBytes(dr).cpu().numpy())
+    plan.close(); plan2.close(); comm.close()
+
+
+def test_rccl_sharded_plan_rejects_uneven_rows(gpu):
+    import ggml_hip as G
+    comm = G.Comm.single()
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 16)
+    a = ga.allocateTensor(G.GGMLType.Q4_0, [64, 8])
+    b = ga.allocateTensor(G.GGMLType.F32, [1, 64])
+    d = ga.allocateTensor(G.GGMLType.F32, [1, 16])  # A holds 8 rows of a 16-row dst at P = 1
+    with pytest.raises(G.IllegalArgumentException):
+        G.ShardedMulMatPlan(comm, ga, [(a, b, d)])
+    comm.close()
