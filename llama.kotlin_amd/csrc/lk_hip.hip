@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "lk_kernels.hpp"
+#include "lk_mfma32.hpp"
 #include "../../include/lk_gguf.h"
 
 using namespace lk;
@@ -565,7 +566,58 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   return LK_OK;
 }
 
+// gemm_q32_kernel (lk_mfma32.hpp): Q4_0 / Q4_1, 17 <= N <= 32, K % 256 == 0, weight rows and base
+// 16-byte aligned, B dense (nb[0] == 4, nb[1] == 4N, N % 4 == 0) and 16-byte aligned.
+bool q32_eligible(const lk_tensor *a, const lk_tensor *b, const Checked &c) {
+  // lab only (LK_Q32=1): measured slower than gemm_skinny_pair_kernel on C3 (28 vs 22 us per call:
+  // an 8 us prologue and ~86 VALU per 32-row block), so off by default
+  static const int mode = [] { const char *e = getenv("LK_Q32"); return e ? atoi(e) : 0; }();
+  if (!mode || (a->type != LK_TYPE_Q4_0 && a->type != LK_TYPE_Q4_1)) return false;
+  if (c.N < (mode == 2 ? 2 : 17) || c.N > 32 || c.N % 4 || c.K % 256) return false;
+  const uint64_t rb = (uint64_t)(c.K / 32) * block_bytes(a->type);
+  const uintptr_t abase = (uintptr_t)a->data + a->data_offset, bbase = (uintptr_t)b->data + b->data_offset;
+  return abase % 16 == 0 && rb % 16 == 0 && rb * 32 < (1ull << 31) && bbase % 16 == 0 && b->nb[0] == 4 &&
+         b->nb[1] == 4 * (uint64_t)c.N;
+}
+
+template <int QT>
+int launch_q32_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  using QG = Q32Geom<QT>;
+  GemmScratch &S = gemm_scratch();
+  Q32Args g{};
+  g.a = (const uint8_t *)a->data + a->data_offset;
+  g.b = (const uint8_t *)b->data + b->data_offset;
+  g.dst = (uint8_t *)dst->data + dst->data_offset;
+  g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
+  g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
+  const int nblk = g.K / 32;
+  const int slices = (nblk + QG::SB - 1) / QG::SB;
+  const int ntile = (g.M + 31) / 32;
+  // one workgroup per CU: ranges x slices <= CUs, so every task runs in the first round
+  int ranges = std::max(1, std::min(ntile, cu_count() / slices));
+  g.tiles_per_range = (ntile + ranges - 1) / ranges;
+  ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
+  g.slices = slices;
+  if (slices > 1) {
+    const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 32 * sizeof(float));
+    if (rc) return rc;
+    g.partial = (float *)S.partial;
+  }
+  g.tasks = ranges * slices;
+  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  hipLaunchKernelGGL((gemm_q32_kernel<QT>), dim3(grid), dim3(QG::NW * 64), QG::LDS, st, g);
+  if (slices > 1) {
+    const int64_t threads = (int64_t)g.M * (32 / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
+                       slices, g.M, g.N, 32, g.dst, g.d_nb0, g.d_nb1);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
 int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  if (q32_eligible(a, b, c))
+    return a->type == LK_TYPE_Q4_0 ? launch_q32_t<LK_TYPE_Q4_0>(a, b, dst, c, st) : launch_q32_t<LK_TYPE_Q4_1>(a, b, dst, c, st);
   SkinnyArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
   g.b = (const uint8_t *)b->data + b->data_offset;

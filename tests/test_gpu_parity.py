@@ -420,3 +420,32 @@ def test_c1_f32_512_cubed(gpu, oracle):
     got = ga.tensorBytes(td).cpu().numpy().view(np.float32).reshape(n, n)
     ok, msg = parity_ok(got, ref, noise=acc_noise(np.abs(a.reshape(n, n)), np.abs(x.reshape(n, n))))
     assert ok, msg
+
+
+# 32x32x16 MFMA GEMM for Q4_0 / Q4_1 at 17 <= N <= 32 (N % 4 == 0, K % 256 == 0, dense B):
+# ragged rows, one-slice direct stores (K <= 512), a half slice at the end of K, full C3.
+Q32 = [
+    (257, 4096, 20),    # ragged rows (a 1-row tile), 8 slices
+    (64, 256, 24),      # one half slice: direct stores
+    (100, 512, 28),     # one full slice: direct stores
+    (33, 768, 32),      # a full and a half slice
+    (1000, 11008, 32),  # 43 blocks x 8: the last slice half, many tiles per range
+]
+
+
+@pytest.mark.parametrize("qt", [2, 3], ids=lambda t: QNAME[t])
+@pytest.mark.parametrize("shape", Q32, ids=lambda s: "x".join(map(str, s)))
+def test_q32_gemm_vs_oracle(gpu, oracle, qt, shape, monkeypatch):
+    """gemm_q32_kernel is a lab kernel (LK_Q32=1 routes to it; the library reads the switch once,
+    so this test covers it only when the whole session runs with LK_Q32=1); by default the same
+    shapes run on the skinny kernels."""
+    M, K, N = shape
+    for kind in ("random", "pattern"):
+        q, x = make_inputs(oracle, qt, M, K, N, kind, seed=M + 7 * N)
+        ref = oracle.mat_mul_q(qt, q, M, K, x, tight=True)
+        noise = noise_for(oracle, qt, q, M, K, x)
+        got = gpu_matmul(qt, q, M, K, N, x)
+        ok, msg = parity_ok(got, ref, noise=noise)
+        assert ok, (kind, msg)
+        again = gpu_matmul(qt, q, M, K, N, x)
+        assert np.array_equal(got.view(np.uint32), again.view(np.uint32)), "not deterministic"
