@@ -756,6 +756,27 @@ GenericArgs make_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst,
   return g;
 }
 
+int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st);
+
+bool getenv_flag(const char *name) {  // lab switches, read per call (cheap; A/B only)
+  const char *e = getenv(name);
+  return e && *e && *e != '0';
+}
+
+// F32 x F32 -> F32 on the f32 MFMA (f32_mfma_kernel): any strides; float4 loads of A's rows when
+// they are contiguous and 16-byte aligned.
+int launch_f32_mfma(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  const GenericArgs g = make_generic(a, b, dst, c);
+  const int64_t gx = (c.N + 31) / 32, gy = (c.M + 31) / 32;
+  if (gx > 0x7FFFFFFF || gy > 65535) return launch_generic(a, b, dst, c, st);
+  dim3 grid((unsigned)gx, (unsigned)gy), block(256);
+  const bool v4 = g.a_nb0 == 4 && g.a_nb1 % 16 == 0 && ((uintptr_t)g.a & 15) == 0;
+  if (v4) hipLaunchKernelGGL(f32_mfma_kernel<true>, grid, block, 0, st, g);
+  else hipLaunchKernelGGL(f32_mfma_kernel<false>, grid, block, 0, st, g);
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
 int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   const GenericArgs g = make_generic(a, b, dst, c);
   const int64_t waves = c.M * c.N;
@@ -882,6 +903,7 @@ int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *ds
     return launch_generic(a, b, dst, c, st);
   }
   if (c.path == Path::kKQuantF32) return launch_kquant(a, b, dst, c, st);
+  if (c.path == Path::kF32 && !getenv_flag("LK_NO_F32_MFMA")) return launch_f32_mfma(a, b, dst, c, st);
   if (gemv_eligible(a, b, dst, c)) return run_single_gemv(a, b, dst, c, st);
   if (gemm_eligible(c)) return skinny_eligible(a, c) ? launch_skinny(a, b, dst, c, st) : launch_gemm(a, b, dst, c, st);
   return launch_generic(a, b, dst, c, st);

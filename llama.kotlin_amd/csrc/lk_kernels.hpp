@@ -2088,17 +2088,20 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restr
   if (idx >= (int64_t)M * c4) return;
   const int64_t m = idx / c4;
   const int n0 = (int)(idx % c4) * 4;
-  // slabs in slice order (deterministic); eight loads in flight at a time instead of one
-  // dependent L2 round trip per slice
-  f32x4 s = *(const f32x4 *)(P + m * N16 + n0);
-  for (int b = 1; b < slices; b += 8) {
-    f32x4 v[8];
+  // slabs in slice order (deterministic); all of a group's loads (up to 16) in flight at once,
+  // the first slab's included, instead of one dependent round trip per slice
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < slices; b += 16) {
+    f32x4 v[16];
 #pragma unroll
-    for (int i = 0; i < 8; i++)
-      if (b + i < slices) v[i] = *(const f32x4 *)(P + ((int64_t)(b + i) * M + m) * N16 + n0);
+    for (int i = 0; i < 16; i++)
+      if (b + i < slices) v[i] = __builtin_nontemporal_load((const f32x4 *)(P + ((int64_t)(b + i) * M + m) * N16 + n0));
 #pragma unroll
-    for (int i = 0; i < 8; i++)
-      if (b + i < slices) { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
+    for (int i = 0; i < 16; i++)
+      if (b + i < slices) {
+        if (b + i == 0) s = v[i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
+        else { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
+      }
   }
   const float e4[4] = {s.x, s.y, s.z, s.w};
   if (d_nb0 == 4 && n0 + 4 <= N && (((uintptr_t)(dst + m * d_nb1 + n0 * 4)) & 15) == 0) {
@@ -2108,6 +2111,63 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restr
 #pragma unroll
   for (int q = 0; q < 4; q++)
     if (n0 + q < N) *(float *)(dst + m * d_nb1 + (n0 + q) * d_nb0) = e4[q];
+}
+
+// ---- F32 x F32 -> F32 general path on the f32 MFMA (computeMatMul :1530-1543, config C1) ----
+//
+// v_mfma_f32_32x32x2_f32: f32 operands, products exact, each accumulation one f32 rounding (a
+// k-ordered fmaf chain), so the only difference from the reference's sequential sum is the
+// summation order (within the F32 bar). One workgroup per 32x32 output tile, four waves; wave w
+// takes K chunks w, w + 4, ... of 128: MFMA step s contracts k = {c + s, c + 64 + s} (lane half
+// h supplies k = c + 64h + s), so a lane's A operand is 64 consecutive floats of its row (16
+// float4 loads when rows are 16-byte aligned). The four waves' tiles are added in wave order
+// through LDS (deterministic).
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+template <bool V4>
+__global__ __launch_bounds__(256) void f32_mfma_kernel(GenericArgs g) {
+  __shared__ float red[4][16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t i0 = (int64_t)blockIdx.y * 32, j0 = (int64_t)blockIdx.x * 32;
+  const int64_t i = i0 + r, j = j0 + r;
+  const bool iok = i < g.M, jok = j < g.N;
+  f32x16_t acc = {};
+  for (int64_t c = (int64_t)wave * 128; c < g.K; c += 4 * 128) {
+    const int64_t kb = c + 64 * h;
+    float av[64], bv[64];
+    if (V4 && iok && c + 128 <= g.K) {
+      const f32x4 *ap = (const f32x4 *)(g.a + i * g.a_nb1 + kb * 4);
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const f32x4 t = ap[q];
+        av[4 * q] = t.x; av[4 * q + 1] = t.y; av[4 * q + 2] = t.z; av[4 * q + 3] = t.w;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 64; s++)
+        av[s] = (iok && kb + s < g.K) ? *(const float *)(g.a + i * g.a_nb1 + (kb + s) * g.a_nb0) : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 64; s++)
+      bv[s] = (jok && kb + s < g.K) ? *(const float *)(g.b + j * g.b_nb0 + (kb + s) * g.b_nb1) : 0.f;
+#pragma unroll
+    for (int s = 0; s < 64; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; q++) red[wave][q][lane] = acc[q];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      float v = red[0][q][lane];
+      v += red[1][q][lane];
+      v += red[2][q][lane];
+      v += red[3][q][lane];
+      const int64_t ii = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;  // C row (A row), column = lane r (B column)
+      if (ii < g.M && jok) *(float *)(g.dst + j * g.d_nb0 + ii * g.d_nb1) = v;
+    }
+  }
 }
 
 // ---- generic path (any K, any byte strides, ragged blocks) ----------------------
