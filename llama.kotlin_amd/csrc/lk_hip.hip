@@ -24,6 +24,7 @@
 
 #include "lk_kernels.hpp"
 #include "lk_mfma32.hpp"
+#include "lk_skinny.hpp"
 #include "../../include/lk_gguf.h"
 
 using namespace lk;
@@ -615,7 +616,72 @@ int launch_q32_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const C
   return LK_OK;
 }
 
+// gemm_sk_kernel (lk_skinny.hpp): Q4_0 / Q4_1, 2 <= N <= 32, after skinny_eligible. The
+// activations are split once into MFMA fragments (xsplit_kernel), then the split-K GEMM, then
+// the ordered slab reduction.
+template <int QT, int NT, bool SOLO>
+int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  using SG = SkGeom<QT, NT>;
+  using SG1 = Sk1Geom<QT, NT>;
+  GemmScratch &S = gemm_scratch();
+  const int64_t nblk = c.K / 32, ntx = (c.N + 15) / 16;
+  const size_t fb = (size_t)ntx * nblk * kXSplits * 64 * 16, sb = (size_t)nblk * ntx * 16 * sizeof(float);
+  int rc = grow(&S.frag, &S.frag_bytes, fb + sb);
+  if (rc) return rc;
+  XSplitArgs xa{};
+  xa.b = (const uint8_t *)b->data + b->data_offset;
+  xa.b_nb0 = b->nb[0]; xa.b_nb1 = b->nb[1];
+  xa.N = c.N; xa.K = c.K;
+  xa.frag = (u32x4 *)S.frag;
+  xa.xsum = (float *)((uint8_t *)S.frag + fb);
+  xa.mult = 1.f;
+  xa.q4_order = 2;
+  SkArgs g{};
+  g.a = (const uint8_t *)a->data + a->data_offset;
+  g.frag = xa.frag;
+  g.xsum = xa.xsum;
+  g.dst = (uint8_t *)dst->data + dst->data_offset;
+  g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
+  g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
+  const int slices = (int)((nblk + SG::SB - 1) / SG::SB);
+  const int ntile = (g.M + 15) / 16;
+  int ranges = std::max(1, std::min(ntile, (cu_count() + slices - 1) / slices));
+  g.tiles_per_range = (ntile + ranges - 1) / ranges;
+  ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
+  g.slices = slices;
+  if (slices > 1) {
+    rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
+    if (rc) return rc;
+    g.partial = (float *)S.partial;
+  }
+  g.tasks = ranges * slices;
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  if (SOLO) hipLaunchKernelGGL((gemm_sk1_kernel<QT, NT>), dim3(grid), dim3(SG1::NW * 64), SG1::LDS, st, g);
+  else hipLaunchKernelGGL((gemm_sk_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
+  if (slices > 1) {
+    const int64_t threads = (int64_t)g.M * (16 * NT / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
+                       slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
 int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  // Lab (LK_SK=1: gemm_sk_kernel, wave pairs; LK_SK=2: gemm_sk1_kernel, one wave per SIMD; both
+  // lk_skinny.hpp): parity-green, measured slower than the kernels below on C3 (27 / 29 vs 23 us
+  // per call), so off by default; DESIGN.md §3 has the timeline.
+  static const int sk = [] { const char *e = getenv("LK_SK"); return e ? atoi(e) : 0; }();
+  if (sk && (a->type == LK_TYPE_Q4_0 || a->type == LK_TYPE_Q4_1)) {
+    const bool one = c.N <= 16;
+#define LK_SKL(S) \
+    if (a->type == LK_TYPE_Q4_0) return one ? launch_sk_t<LK_TYPE_Q4_0, 1, S>(a, b, dst, c, st) : launch_sk_t<LK_TYPE_Q4_0, 2, S>(a, b, dst, c, st); \
+    return one ? launch_sk_t<LK_TYPE_Q4_1, 1, S>(a, b, dst, c, st) : launch_sk_t<LK_TYPE_Q4_1, 2, S>(a, b, dst, c, st);
+    if (sk == 2) { LK_SKL(true) }
+    LK_SKL(false)
+#undef LK_SKL
+  }
   if (q32_eligible(a, b, c))
     return a->type == LK_TYPE_Q4_0 ? launch_q32_t<LK_TYPE_Q4_0>(a, b, dst, c, st) : launch_q32_t<LK_TYPE_Q4_1>(a, b, dst, c, st);
   SkinnyArgs g{};

@@ -723,7 +723,7 @@ struct XSplitArgs {
   u32x4 *frag;        // [ntx][nblk][kXSplits][64] x 16 B
   float *xsum;        // [nblk][N16]: mult · Σ_block x
   float mult;
-  int32_t q4_order;   // 1: k order (0,2,4,6,1,3,5,7) within each 8
+  int32_t q4_order;   // 1: k order (0,2,4,6,1,3,5,7) within each 8; 2: (0,4,1,5,2,6,3,7) (lk_skinny.hpp)
 };
 
 // One wave per (x-tile, block).
@@ -739,11 +739,12 @@ __global__ __launch_bounds__(256) void xsplit_kernel(XSplitArgs g) {
   float part = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    const int kk = g.q4_order ? ((j & 3) * 2 + (j >> 2)) : j;
+    const int kk = g.q4_order == 2 ? ((j >> 1) + 4 * (j & 1)) : g.q4_order ? ((j & 3) * 2 + (j >> 2)) : j;
     v[j] = (n < g.N) ? *(const float *)(g.b + n * g.b_nb0 + (k0 + kk) * g.b_nb1) : 0.f;
     part += v[j];
   }
   uint32_t hi[4], lo[4];
+  float hsum = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {
     uint32_t h[2], l[2];
@@ -755,12 +756,16 @@ __global__ __launch_bounds__(256) void xsplit_kernel(XSplitArgs g) {
       br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even (r is finite, |r| < 2^-7·|x|)
       h[q] = bx;
       l[q] = br;
+      // q4_order 2 (lk_skinny.hpp) cancels a 136-fold offset against this sum: take it over the
+      // split itself, hi + lo, so the split's own error is not amplified
+      if (g.q4_order == 2) hsum += __builtin_bit_cast(float, bx & 0xFFFF0000u) + __builtin_bit_cast(float, br & 0xFFFF0000u);
     }
     hi[j / 2] = __builtin_amdgcn_perm(h[1], h[0], 0x07060302u);
     lo[j / 2] = __builtin_amdgcn_perm(l[1], l[0], 0x07060302u);
   }
   g.frag[(idx * kXSplits + 0) * 64 + lane] = u32x4{hi[0], hi[1], hi[2], hi[3]};
   g.frag[(idx * kXSplits + 1) * 64 + lane] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+  if (g.q4_order == 2) part = hsum;
   part += __shfl_xor(part, 16, kWave);
   part += __shfl_xor(part, 32, kWave);
   if (lane < 16) g.xsum[kb * (ntx * 16) + n] = g.mult * part;

@@ -1,0 +1,648 @@
+// lk_skinny.hpp — Q4_0 / Q4_1 x F32 at 2 <= N <= 32 (config C3's batch 32) on gfx950.
+//
+// computeMatMul's quantized dots (core/GGMLComputeOps.kt:70-145, dispatched at :1448-1480) for
+// a few activation columns, on v_mfma_f32_16x16x32_bf16. Arithmetic:
+//
+//  * Activations as bf16 hi + lo (|x − hi − lo| ≤ 2⁻¹⁷|x|), split once per call by xsplit_kernel
+//    into 1-KB MFMA operand fragments, plus S = Σx per (block, column).
+//  * Codes as the exact bf16 128 + n, two per v_and_or_b32: (u & 0x000F000F) | 0x43004300 (bf16
+//    0x43 0x0n = 128 + n), so a lane's 8 codes cost 7 VALU (k order 0,4,1,5,2,6,3,7, which
+//    xsplit writes the activations in). The MFMA gives p = Σ (128 + n)·x per block.
+//  * Per block: acc += d·p (packed f32 FMAs). The offsets fold into one f32 term per block,
+//    e·S with e = −136·d (Q4_0: d·(n − 8) = d·(128 + n) − 136·d) or e = m − 128·d (Q4_1:
+//    d·n + m), summed over a wave's 8 blocks by two v_mfma_f32_16x16x4_f32 per 16-column tile
+//    (exact f32 products) straight into the accumulators.
+//
+// On gfx950 a SIMD issues one wave64 VALU instruction per ~4.3 cycles whether one or two waves
+// share it (tools/lab/valu_rate.hip), so the VALU count per block, not latency, sets the pace:
+// 8 + 1 + NT·2 VALU per block here against ~25 for the fp8-conversion decode with scalar FMAs.
+//
+// Schedule: workgroup = (row range, K slice of 16 blocks), 8 waves; wave (stream p = w % 4,
+// half h = w / 4) streams 16-row tiles t0 + p + 4i, its half's eight blocks of each row through
+// its own LDS-DMA ring. The slice's fragments and block sums are landed in LDS once by LDS-DMA
+// and read into VGPRs (each wave: its 8 blocks). The h = 1 wave (issue priority 1) hands its
+// accumulators to its partner through LDS (ready / ack flags, 2 parities); the h = 0 wave adds
+// them one unit later, in a fixed order, and stores (partial slab per slice, reduced in slice
+// order: deterministic).
+#pragma once
+
+#include "lk_kernels.hpp"
+
+namespace lk {
+
+// Lab knobs (compile time): LK_SK_PRIO raises the h = 1 wave's issue priority (it is the younger
+// wave of its SIMD and otherwise loses VALU arbitration, while its partner waits in the hand-off).
+#ifndef LK_SK_PRIO
+#define LK_SK_PRIO 1
+#endif
+
+template <int QT, int NT> struct SkGeom {
+  static constexpr int NW = 8;                          // 4 streams x 2 halves
+  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr int SB = 16, SBH = 8;                // blocks per slice / per half
+  static constexpr int RPH = SBH * BB;                  // bytes of a half row piece (144 / 160)
+  static constexpr int PPH = RPH / 16;                  // 16-B cells per half row
+  static constexpr int L = (16 * PPH + 63) / 64;        // DMA instructions per half unit
+  static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : 3;
+  static constexpr int SLOT = L * 1024;
+  static constexpr int XI = SB * NT * kXSplits;         // 1-KB activation fragments of the slice
+  static constexpr int XF = XI * 1024;
+  static constexpr int TB = SB * 16 * NT * 4;           // S = Σx per (block, column)
+  static constexpr int TI = TB / 1024;                  // its DMA instructions
+  static constexpr int EB = 2 * 4 * NT * 64 * 16;       // accumulator hand-off, 2 parities x 4 pairs
+  static constexpr int FB = 64;                         // ready[4][2], ack[4] (ints)
+  static constexpr int DFIT = (kLdsBytes - XF - TB - EB - FB) / (NW * SLOT);
+  static constexpr int D = DFIT > 4 ? 4 : DFIT;         // ring depth (half units per wave)
+  static constexpr int LDS = XF + TB + EB + FB + NW * D * SLOT;
+  static constexpr int MAXW = L * (D - 1) + D * NT;     // largest vmcnt a wait needs
+  static_assert(RPH % 16 == 0, "half row pieces");
+  static_assert(TB % 1024 == 0, "T DMA");
+  static_assert(D >= 2, "ring must double-buffer");
+  static_assert(LDS <= kLdsBytes, "LDS");
+  static_assert(MAXW < 64, "vmcnt");
+};
+
+struct SkArgs {
+  const uint8_t *a;        // weights (buffer base + dataOffset), rows RB bytes apart
+  const u32x4 *frag;       // xsplit_kernel fragments [ntx][nblk][2][64]
+  const float *xsum;       // [nblk][16·ntx]: Σx per (block, column) (Q4_1)
+  uint8_t *dst;            // dst(n, m) at n·d_nb0 + m·d_nb1
+  int64_t d_nb0, d_nb1;
+  float *partial;          // [slices][M][16·NT] when slices > 1
+  int32_t M, N, K;
+  int32_t slices, tiles_per_range, tasks;  // tasks = ranges·slices (the grid is padded to 8)
+};
+
+// LDS-typed pointers throughout (no generic -> LDS conversions, no null checks on them).
+typedef LK_LDS uint8_t lu8;
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+// dma16 (lk_kernels.hpp) with the LDS destination as an LDS pointer: M0 is its 32-bit offset.
+template <bool NT>
+__device__ __forceinline__ void dma16l(const void *sbase, uint32_t vofs, const lu8 *lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_dst);
+  const uint64_t sb = (uint64_t)(uintptr_t)sbase;
+  const uint32_t sb_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
+  const uint32_t sb_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+  sbase = (const void *)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo);
+  if constexpr (NT) asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
+  else asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+__device__ __forceinline__ int ldsl_ld(const LK_LDS int *p) {
+  asm volatile("" ::: "memory");
+  const int v = *(volatile const LK_LDS int *)p;
+  asm volatile("" ::: "memory");
+  return v;
+}
+__device__ __forceinline__ void ldsl_st(LK_LDS int *p, int v) {
+  asm volatile("" ::: "memory");
+  *(volatile LK_LDS int *)p = v;
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ uint32_t lds32(const lu8 *p) { return *(const LK_LDS uint32_t *)p; }
+
+// The WPB dwords of block B for lane (row m = lane & 15, group g = lane >> 4): bm = slot + m·RPH,
+// bg = bm + 4g (as skinny_read in lk_kernels.hpp).
+template <int QT, int B, int WPB>
+__device__ __forceinline__ void sk_read(const lu8 *bm, const lu8 *bg, uint32_t (&w)[WPB]) {
+  constexpr int OB = B * QTraits<QT>::BB;
+  if constexpr (QT == LK_TYPE_Q4_1) {  // (d, m) dword; codes at +4 + 4g
+    w[0] = lds32(bm + OB);
+    w[1] = lds32(bg + OB + 4);
+  } else if constexpr ((OB & 3) == 0) {  // d lo; codes at +2 + 4g: two dwords, realigned by 2
+    w[0] = lds32(bm + OB);
+    w[1] = lds32(bg + OB);
+    w[2] = lds32(bg + OB + 4);
+  } else {  // d in the high half of the dword before; codes aligned
+    w[0] = lds32(bm + OB - 2);
+    w[1] = lds32(bg + OB + 2);
+    w[2] = 0;
+  }
+}
+template <int QT, int WPB, int B, int NBW>
+__device__ __forceinline__ void sk_read_all(const lu8 *bm, const lu8 *bg, uint32_t (&w)[NBW][WPB]) {
+  if constexpr (B < NBW) {
+    sk_read<QT, B, WPB>(bm, bg, w[B]);
+    sk_read_all<QT, WPB, B + 1, NBW>(bm, bg, w);
+  }
+}
+
+// bf16 codes 128 + n of the 8 nibbles of dword u, slots in k order (0,4,1,5,2,6,3,7).
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(o));  // one VALU (the compiler splits it)
+  return r;
+}
+__device__ __forceinline__ bf16x8 q4_codes_128(uint32_t u) {
+  constexpr uint32_t M = 0x000F000Fu, E = 0x43004300u;
+  uint32_t w[4] = {and_or(u, M, E), and_or(u >> 4, M, E), and_or(u >> 8, M, E), and_or(u >> 12, M, E)};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+// Block B of a unit: codes + scale d from its dwords, 2·NT MFMAs into p.
+template <int QT, int NT, int B, int WPB, int NBW>
+__device__ __forceinline__ void sk_mfma(const uint32_t (&w)[WPB], const u32x4 (&xh)[NBW][NT], const u32x4 (&xl)[NBW][NT],
+                                        f32x4 (&p)[NT], float &s1) {
+  constexpr int OB = B * QTraits<QT>::BB;
+  bf16x8 wf;
+  if constexpr (QT == LK_TYPE_Q4_1) {
+    wf = q4_codes_128(w[1]);
+    s1 = h2f(w[0]);
+  } else if constexpr ((OB & 3) == 0) {
+    wf = q4_codes_128(align2(w[2], w[1]));
+    s1 = h2f(w[0]);
+  } else {
+    wf = q4_codes_128(w[1]);
+    s1 = h2f(w[0] >> 16);
+  }
+#pragma unroll
+  for (int j = 0; j < NT; j++)
+    p[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < NT; j++)
+    p[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p[j], 0, 0, 0);
+}
+
+// acc += d·p as packed FMAs (two per tile: a wave64 v_pk_fma_f32 issues as fast as a v_fma_f32).
+// Masked blocks (past a short slice) have zero activation fragments, so p == 0; d is zeroed
+// too, since the slot bytes there are stale (d may be inf / NaN).
+template <int NT, int B, bool MASK>
+__device__ __forceinline__ void sk_scale(const f32x4 (&p)[NT], float s1, int nb, f32x4 (&acc)[NT]) {
+  if (MASK && B >= nb) s1 = 0.f;
+  const f2v m1 = {s1, s1};
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    const f2v a0 = __builtin_elementwise_fma(m1, f2v{p[j].x, p[j].y}, f2v{acc[j].x, acc[j].y});
+    const f2v a1 = __builtin_elementwise_fma(m1, f2v{p[j].z, p[j].w}, f2v{acc[j].z, acc[j].w});
+    acc[j] = f32x4{a0.x, a0.y, a1.x, a1.y};
+  }
+}
+
+// Scheduling hint for a unit's block section (one basic block): alternate each MFMA with a few
+// VALU instructions, so the decode of the next block and the scaling of the previous one issue in
+// the MFMA gaps instead of as one VALU run ahead of a dependent MFMA chain. LK_SK_SCHED = VALU per
+// MFMA (0: leave it to the compiler).
+#ifndef LK_SK_SCHED
+#define LK_SK_SCHED 3
+#endif
+template <int NMFMA>
+__device__ __forceinline__ void sk_interleave() {
+#if LK_SK_SCHED > 0
+#pragma unroll
+  for (int i = 0; i < NMFMA; i++) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // one MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, LK_SK_SCHED, 0);   // then VALU
+  }
+#endif
+}
+
+// All NBW blocks of a unit, pipelined: block B's MFMAs go out before block B − 1 is scaled in.
+template <int QT, int NT, int WPB, bool MASK, int B, int NBW>
+__device__ __forceinline__ void sk_blocks(const uint32_t (&w)[NBW][WPB], const u32x4 (&xh)[NBW][NT], const u32x4 (&xl)[NBW][NT],
+                                          int nb, f32x4 (&pp)[NT], float ps1, f32x4 (&acc)[NT]) {
+  if constexpr (B < NBW) {
+    f32x4 p[NT];
+    float s1;
+    sk_mfma<QT, NT, B, WPB, NBW>(w[B], xh, xl, p, s1);
+    if constexpr (B > 0) sk_scale<NT, B - 1, MASK>(pp, ps1, nb, acc);
+    if constexpr (B == NBW - 1) sk_scale<NT, NBW - 1, MASK>(p, s1, nb, acc);
+    else sk_blocks<QT, NT, WPB, MASK, B + 1, NBW>(w, xh, xl, nb, p, s1, acc);
+  }
+}
+
+// Lab timeline (tools/lab/sk_trace.hip defines LK_SK_TRACE): per wave, s_memrealtime at entry,
+// after the barrier, unit 0 landed / computed, loop done; s_memtime cycles summed over the units
+// waiting for the DMA, computing, and in the hand-off.
+#ifdef LK_SK_TRACE
+__device__ uint64_t *lk_sktrace_buf;
+#define LK_SKT_NOW() __builtin_amdgcn_s_memtime()
+#define LK_SKT(slot_, v_)                                                                                  \
+  do {                                                                                                     \
+    uint64_t *tb_ = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_sktrace_buf)[0];   \
+    if (lane == 0 && tb_) tb_[((size_t)blockIdx.x * 8 + wave) * 8 + (slot_)] = (v_);                        \
+  } while (0)
+#else
+#define LK_SKT_NOW() 0ull
+#define LK_SKT(slot_, v_) do {} while (0)
+#endif
+
+template <int QT, int NT>
+__global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
+  using G = SkGeom<QT, NT>;
+  constexpr int BB = G::BB, D = G::D, L = G::L;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int p = wave & 3, h = wave >> 2;
+  lu8 *const sbase = (lu8 *)smem;
+  lu8 *xlds = sbase;                                              // the slice's fragments (tile j, block b, split s)
+  LK_LDS float *tlds = (LK_LDS float *)(sbase + G::XF);           // S: Σx of the slice's blocks
+  LK_LDS f32x4 *xch = (LK_LDS f32x4 *)(sbase + G::XF + G::TB);
+  LK_LDS int *flags = (LK_LDS int *)(sbase + G::XF + G::TB + G::EB);  // ready[p][parity] at 2p + parity, ack[p] at 8 + p
+  lu8 *ring = sbase + G::XF + G::TB + G::EB + G::FB + wave * D * G::SLOT;
+  // XCD-aware task order (speed only): the slices of one row range land on one XCD's L2
+  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+  if (task >= g.tasks) return;  // grid padding (before the barrier: the whole workgroup leaves)
+  [[maybe_unused]] const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+  [[maybe_unused]] uint64_t c_wait = 0, c_comp = 0, c_hand = 0, c_issue = 0;
+  const int slice = task % g.slices, range = task / g.slices;
+  const int nblk = g.K / 32;
+  const int kb0 = slice * G::SB, nb = min(G::SB, nblk - kb0);
+  const int nbh = max(0, min(G::SBH, nb - G::SBH * h));  // this wave's blocks
+  const int64_t RB = (int64_t)nblk * BB;
+  const int ntile = (g.M + 15) / 16;
+  const int t0 = range * g.tiles_per_range, t1 = min(t0 + g.tiles_per_range, ntile);
+  const int nunits = t1 - t0 - p > 0 ? (t1 - t0 - p + 3) / 4 : 0;  // stream p: tiles t0 + p + 4i
+  const int pph = nbh * BB / 16;
+  const int myL = nbh > 0 ? L : 0;
+
+  if (threadIdx.x < 16) flags[threadIdx.x] = 0;  // published by the barrier below
+
+  // half unit u = rows of tile t0 + p + 4u, bytes [kb0·BB + h·RPH, + nbh·BB) of each; cell
+  // q = r·PPH + c lands at slot + 16q (row pitch RPH); cells past the unit re-read cell 0
+  const uint8_t *abase = g.a + (int64_t)kb0 * BB + (int64_t)h * G::RPH;
+  uint32_t rofs[L];
+  int rrow[L];
+#pragma unroll
+  for (int j = 0; j < L; j++) {
+    const int q = j * 64 + lane, r = q / G::PPH, c = q % G::PPH;
+    rrow[j] = min(r, 15);
+    rofs[j] = (uint32_t)((c < pph && r < 16) ? c * 16 : 0);
+  }
+  auto issue = [&](int u, int sl) __attribute__((always_inline)) {
+    const int t = t0 + p + u * 4;
+    const uint8_t *tb = abase + (int64_t)t * 16 * RB;
+    const int rmax = g.M - 1 - t * 16;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
+      dma16l<LK_SKINNY_NT>(tb, vofs, ring + sl * G::SLOT + j * 1024);
+    }
+  };
+
+  // 1. the first weight unit; the slice's activation fragments (and Q4_1 block sums) into LDS,
+  //    spread over the workgroup's waves; the rest of the ring
+  if (myL && nunits > 0) issue(0, 0);
+  for (int i = wave; i < G::XI; i += G::NW) {  // fragment i: tile i / 32, block (i % 32) / 2, split i % 2
+    const int j = i / (2 * G::SB), b = (i % (2 * G::SB)) / 2, sp = i % 2;
+    const int kb = b < nb ? kb0 + b : kb0;      // past a short slice: any valid fragment (masked)
+    dma16l<false>(g.frag, (uint32_t)((((int64_t)j * nblk + kb) * kXSplits + sp) * 1024 + lane * 16), xlds + i * 1024);
+  }
+  {
+    const int n16 = 16 * NT;
+    const int64_t tot = (int64_t)nblk * n16;   // floats in xsum
+    if (wave < G::TI) {
+      int64_t f = (int64_t)kb0 * n16 + 256 * wave + 4 * lane;
+      if (f + 4 > tot) f = 0;                   // past the last block: masked
+      dma16l<false>(g.xsum, (uint32_t)(f * 4), (lu8 *)tlds + wave * 1024);
+    }
+  }
+  if (myL)
+    for (int u = 1; u < min(D, nunits); u++) issue(u, u);
+  // fragments landed (and this wave's unit 0: the DMA before them), flags written; the ring's
+  // later units stay in flight across the bare barrier
+  wait_vmcnt_rt<G::MAXW>(myL * max(0, min(D - 1, nunits - 1)));
+  wait_lgkmcnt0();
+  __builtin_amdgcn_s_barrier();
+  u32x4 xh[8][NT], xl[8][NT];
+#pragma unroll
+  for (int b = 0; b < 8; b++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const LK_LDS u32x4 *xf = (const LK_LDS u32x4 *)(xlds + ((j * G::SB + G::SBH * h + b) * kXSplits) * 1024) + lane;
+      xh[b][j] = xf[0];
+      xl[b][j] = xf[64];
+      if (b >= nbh) {  // zero, so p == 0 exactly for masked blocks
+        xh[b][j] = u32x4{0u, 0u, 0u, 0u};
+        xl[b][j] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  // bias operands: lane (i = lane & 15, k' = lane >> 4) of v_mfma_f32_16x16x4_f32 c holds
+  // S(block 8h + 4c + k', column 16j + i); zero past the wave's blocks
+  float sf[2][NT];
+#pragma unroll
+  for (int c = 0; c < 2; c++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int bl = 4 * c + (lane >> 4);
+      sf[c][j] = bl < nbh ? tlds[(G::SBH * h + bl) * 16 * NT + 16 * j + (lane & 15)] : 0.f;
+    }
+#if LK_SK_PRIO
+  if (h) __builtin_amdgcn_s_setprio(1);
+#endif
+  LK_SKT(1, __builtin_amdgcn_s_memrealtime());
+
+  const int N16 = 16 * NT;
+  // h = 0 collects unit u − 1's partner sums after computing unit u (the partner, at higher issue
+  // priority, is ahead), so neither wave idles while the other computes: the two waves of a SIMD
+  // overlap their VALU / MFMA streams.
+  auto collect = [&](int v, const f32x4 (&mine)[NT]) __attribute__((always_inline)) {
+    [[maybe_unused]] const uint64_t c2 = LK_SKT_NOW();
+    const LK_LDS f32x4 *xb = xch + ((v & 1) * 4 + p) * NT * 64 + lane;
+    while (ldsl_ld(flags + 2 * p + (v & 1)) != v + 1) __builtin_amdgcn_s_sleep(1);
+    f32x4 sum[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) sum[j] = mine[j] + xb[j * 64];
+    ldsl_st(flags + 8 + p, v + 1);
+#ifdef LK_SK_TRACE
+    c_hand += LK_SKT_NOW() - c2;
+#endif
+    // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
+    const int t = t0 + p + v * 4;
+    const int64_t m = (int64_t)t * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int n0 = 16 * j + 4 * (lane >> 4);
+      if (g.slices > 1) {
+        if (m < g.M) *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = sum[j];
+      } else if (m < g.M) {
+        const float e4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+      }
+    }
+  };
+  f32x4 prev[NT];
+  for (int u = 0; u < nunits; u++) {
+    const int slot = u % D;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    [[maybe_unused]] const uint64_t c0 = LK_SKT_NOW();
+    if (myL) {
+      // ops younger than this unit's DMA: its successors already issued, and the stores of the
+      // collections since (h = 0: NT or more per iteration from iteration 1 on)
+      wait_vmcnt_rt<G::MAXW>(myL * min(D - 1, nunits - 1 - u) + (h == 0 ? NT * min(D, max(u - 1, 0)) : 0));
+      asm volatile("" ::: "memory");
+#ifdef LK_SK_TRACE
+      const uint64_t c1 = LK_SKT_NOW();
+      c_wait += c1 - c0;
+      if (u == 0) LK_SKT(2, __builtin_amdgcn_s_memrealtime());
+#endif
+      uint32_t wd[8][G::WPB];
+      uint32_t eb[2];  // the header (d, and m for Q4_1) of block 4c + (lane >> 4) of the lane's row
+      {
+        const lu8 *bm = ring + slot * G::SLOT + (lane & 15) * G::RPH;
+        const lu8 *bg = bm + 4 * (lane >> 4);
+        sk_read_all<QT, G::WPB, 0, 8>(bm, bg, wd);
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+          const lu8 *hp = bm + (4 * c + (lane >> 4)) * BB;
+          if constexpr (QT == LK_TYPE_Q4_1) eb[c] = lds32(hp);
+          else eb[c] = *(const LK_LDS uint16_t *)hp;
+        }
+        asm volatile("" ::: "memory");
+      }
+      f32x4 pp[NT];
+#ifdef LK_SK_NOCOMP  // lab: the skeleton without decode / MFMAs
+      acc[0].x += __builtin_bit_cast(float, wd[0][0] ^ wd[7][1]);
+#else
+      if (nbh == 8) {
+        sk_blocks<QT, NT, G::WPB, false, 0, 8>(wd, xh, xl, nbh, pp, 0.f, acc);
+        sk_interleave<8 * 2 * NT>();
+      } else {
+        sk_blocks<QT, NT, G::WPB, true, 0, 8>(wd, xh, xl, nbh, pp, 0.f, acc);
+      }
+#endif
+      // the offsets: acc += Σ_b e_b·S_b over the 8 blocks (f32 MFMA, K = 4 blocks each)
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        float e;
+        if constexpr (QT == LK_TYPE_Q4_1) e = fmaf(-128.f, h2f(eb[c]), h2f(eb[c] >> 16));
+        else e = -136.f * h2f(eb[c]);
+        if (4 * c + (lane >> 4) >= nbh) e = 0.f;  // stale header bytes past the wave's blocks
+#pragma unroll
+        for (int j = 0; j < NT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(sf[c][j], e, acc[j], 0, 0, 0);
+      }
+      wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
+#ifdef LK_SK_TRACE
+      const uint64_t c3 = LK_SKT_NOW();
+#endif
+      if (u + D < nunits) issue(u + D, slot);
+#ifdef LK_SK_TRACE
+      c_issue += LK_SKT_NOW() - c3;
+      c_comp += LK_SKT_NOW() - c1;
+      if (u == 0) LK_SKT(3, __builtin_amdgcn_s_memrealtime());
+#endif
+    }
+    if (h == 1) {
+      [[maybe_unused]] const uint64_t c2 = LK_SKT_NOW();
+      // the partner has consumed unit u − 2 (this parity's previous contents)
+      LK_LDS f32x4 *xb = xch + ((u & 1) * 4 + p) * NT * 64 + lane;
+      while (ldsl_ld(flags + 8 + p) < u - 1) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int j = 0; j < NT; j++) xb[j * 64] = acc[j];
+      ldsl_st(flags + 2 * p + (u & 1), u + 1);
+#ifdef LK_SK_TRACE
+      c_hand += LK_SKT_NOW() - c2;
+#endif
+    } else {
+      if (u > 0) collect(u - 1, prev);
+#pragma unroll
+      for (int j = 0; j < NT; j++) prev[j] = acc[j];
+    }
+  }
+  if (h == 0 && nunits > 0) collect(nunits - 1, prev);
+  LK_SKT(0, c_issue);
+  LK_SKT(4, __builtin_amdgcn_s_memrealtime());
+  LK_SKT(5, c_wait);
+  LK_SKT(6, c_comp);
+  LK_SKT(7, c_hand);
+  wait_vmcnt<0>();
+}
+
+// ---- one wave per SIMD: 16 blocks per wave, no hand-off ----------------------------------------
+//
+// gemm_sk1_kernel: 4 waves (one per SIMD, up to 512 registers each); wave p streams 16-row tiles
+// t0 + p + 4i of its workgroup's row range over the whole 16-block K slice: a unit is 16 rows x
+// 16 blocks (288 / 320 B per row, one pad cell per row so the 16 rows' dwords fall in distinct
+// banks), landed by the wave's own LDS-DMA ring. With the VALU per block at 8 + 1 + NT·2 the
+// lone wave issues its MFMAs and VALU back to back; nothing waits on a partner.
+template <int QT, int NT> struct Sk1Geom {
+  static constexpr int NW = 4;
+  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr int SB = 16;                          // blocks per slice (= per wave)
+  static constexpr int RP = SB * BB;                     // row bytes of a unit (288 / 320)
+  static constexpr int PPR = RP / 16;                    // 16-B cells per row
+  static constexpr int PITCH = RP + 16;                  // LDS row pitch: one pad cell
+  static constexpr int L = (16 * (PPR + 1) + 63) / 64;   // DMA instructions per unit
+  static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : 3;
+  static constexpr int SLOT = L * 1024;
+  static constexpr int XI = SB * NT * kXSplits;
+  static constexpr int XF = XI * 1024;
+  static constexpr int TB = SB * 16 * NT * 4;
+  static constexpr int TI = TB / 1024;
+  static constexpr int DFIT = (kLdsBytes - XF - TB) / (NW * SLOT);
+  static constexpr int D = DFIT > 4 ? 4 : DFIT;
+  static constexpr int LDS = XF + TB + NW * D * SLOT;
+  static constexpr int MAXW = L * (D - 1) + D * NT;
+  static_assert(RP % 16 == 0, "row pieces");
+  static_assert(TB % 1024 == 0, "T DMA");
+  static_assert(D >= 2, "ring must double-buffer");
+  static_assert(LDS <= kLdsBytes, "LDS");
+  static_assert(MAXW < 64, "vmcnt");
+};
+
+template <int QT, int NT>
+__global__ __launch_bounds__(256, 1) void gemm_sk1_kernel(SkArgs g) {
+  using G = Sk1Geom<QT, NT>;
+  constexpr int BB = G::BB, D = G::D, L = G::L, SB = G::SB;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  lu8 *const sbase = (lu8 *)smem;
+  lu8 *xlds = sbase;
+  LK_LDS float *tlds = (LK_LDS float *)(sbase + G::XF);
+  lu8 *ring = sbase + G::XF + G::TB + wave * D * G::SLOT;
+  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+  if (task >= g.tasks) return;
+  LK_SKT(0, __builtin_amdgcn_s_memrealtime());
+  [[maybe_unused]] uint64_t c_wait = 0, c_comp = 0, c_hand = 0;
+  const int slice = task % g.slices, range = task / g.slices;
+  const int nblk = g.K / 32;
+  const int kb0 = slice * SB, nb = min(SB, nblk - kb0);
+  const int64_t RB = (int64_t)nblk * BB;
+  const int ntile = (g.M + 15) / 16;
+  const int t0 = range * g.tiles_per_range, t1 = min(t0 + g.tiles_per_range, ntile);
+  const int nunits = t1 - t0 - wave > 0 ? (t1 - t0 - wave + 3) / 4 : 0;
+  const int ppr = nb * BB / 16;
+
+  const uint8_t *abase = g.a + (int64_t)kb0 * BB;
+  uint32_t rofs[L];
+  int rrow[L];
+#pragma unroll
+  for (int j = 0; j < L; j++) {
+    const int q = j * 64 + lane, r = q / (G::PPR + 1), c = q % (G::PPR + 1);
+    rrow[j] = min(r, 15);
+    rofs[j] = (uint32_t)((c < ppr && r < 16) ? c * 16 : 0);
+  }
+  auto issue = [&](int u, int sl) __attribute__((always_inline)) {
+    const int t = t0 + wave + u * 4;
+    const uint8_t *tb = abase + (int64_t)t * 16 * RB;
+    const int rmax = g.M - 1 - t * 16;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
+      dma16l<LK_SKINNY_NT>(tb, vofs, ring + sl * G::SLOT + j * 1024);
+    }
+  };
+  if (nunits > 0) issue(0, 0);
+  for (int i = wave; i < G::XI; i += G::NW) {
+    const int j = i / (2 * SB), b = (i % (2 * SB)) / 2, sp = i % 2;
+    const int kb = b < nb ? kb0 + b : kb0;
+    dma16l<false>(g.frag, (uint32_t)((((int64_t)j * nblk + kb) * kXSplits + sp) * 1024 + lane * 16), xlds + i * 1024);
+  }
+  {
+    const int n16 = 16 * NT;
+    const int64_t tot = (int64_t)nblk * n16;
+    if (wave < G::TI) {
+      int64_t f = (int64_t)kb0 * n16 + 256 * wave + 4 * lane;
+      if (f + 4 > tot) f = 0;
+      dma16l<false>(g.xsum, (uint32_t)(f * 4), (lu8 *)tlds + wave * 1024);
+    }
+  }
+  for (int u = 1; u < min(D, nunits); u++) issue(u, u);
+  wait_vmcnt_rt<G::MAXW>(L * max(0, min(D - 1, nunits - 1)));
+  __builtin_amdgcn_s_barrier();
+  u32x4 xh[SB][NT], xl[SB][NT];
+#pragma unroll
+  for (int b = 0; b < SB; b++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const LK_LDS u32x4 *xf = (const LK_LDS u32x4 *)(xlds + ((j * SB + b) * kXSplits) * 1024) + lane;
+      xh[b][j] = xf[0];
+      xl[b][j] = xf[64];
+      if (b >= nb) {
+        xh[b][j] = u32x4{0u, 0u, 0u, 0u};
+        xl[b][j] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  float sf[4][NT];
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int bl = 4 * c + (lane >> 4);
+      sf[c][j] = bl < nb ? tlds[bl * 16 * NT + 16 * j + (lane & 15)] : 0.f;
+    }
+  LK_SKT(1, __builtin_amdgcn_s_memrealtime());
+
+  const int N16 = 16 * NT;
+  for (int u = 0; u < nunits; u++) {
+    const int slot = u % D;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    [[maybe_unused]] const uint64_t c0 = LK_SKT_NOW();
+    // ops younger than this unit's DMA: its successors already issued, and the stores since
+    wait_vmcnt_rt<G::MAXW>(L * min(D - 1, nunits - 1 - u) + NT * min(u, D));
+    asm volatile("" ::: "memory");
+#ifdef LK_SK_TRACE
+    const uint64_t c1 = LK_SKT_NOW();
+    c_wait += c1 - c0;
+    if (u == 0) LK_SKT(2, __builtin_amdgcn_s_memrealtime());
+#endif
+    uint32_t wd[SB][G::WPB];
+    uint32_t eb[4];
+    {
+      const lu8 *bm = ring + slot * G::SLOT + (lane & 15) * G::PITCH;
+      const lu8 *bg = bm + 4 * (lane >> 4);
+      sk_read_all<QT, G::WPB, 0, SB>(bm, bg, wd);
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const lu8 *hp = bm + (4 * c + (lane >> 4)) * BB;
+        if constexpr (QT == LK_TYPE_Q4_1) eb[c] = lds32(hp);
+        else eb[c] = *(const LK_LDS uint16_t *)hp;
+      }
+      asm volatile("" ::: "memory");
+    }
+    f32x4 pp[NT];
+    if (nb == SB) {
+      sk_blocks<QT, NT, G::WPB, false, 0, SB>(wd, xh, xl, nb, pp, 0.f, acc);
+      sk_interleave<SB * 2 * NT>();
+    } else {
+      sk_blocks<QT, NT, G::WPB, true, 0, SB>(wd, xh, xl, nb, pp, 0.f, acc);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      float e;
+      if constexpr (QT == LK_TYPE_Q4_1) e = fmaf(-128.f, h2f(eb[c]), h2f(eb[c] >> 16));
+      else e = -136.f * h2f(eb[c]);
+      if (4 * c + (lane >> 4) >= nb) e = 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(sf[c][j], e, acc[j], 0, 0, 0);
+    }
+    wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
+    if (u + D < nunits) issue(u + D, slot);
+#ifdef LK_SK_TRACE
+    c_comp += LK_SKT_NOW() - c1;
+    if (u == 0) LK_SKT(3, __builtin_amdgcn_s_memrealtime());
+#endif
+    const int t = t0 + wave + u * 4;
+    const int64_t m = (int64_t)t * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int n0 = 16 * j + 4 * (lane >> 4);
+      if (g.slices > 1) {
+        if (m < g.M) *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = acc[j];
+      } else if (m < g.M) {
+        const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+      }
+    }
+  }
+  LK_SKT(4, __builtin_amdgcn_s_memrealtime());
+  LK_SKT(5, c_wait);
+  LK_SKT(6, c_comp);
+  LK_SKT(7, c_hand);
+  wait_vmcnt<0>();
+}
+#undef LK_SKT
+#undef LK_SKT_NOW
+
+}  // namespace lk

@@ -346,6 +346,8 @@ SKINNY = [
     (257, 4096, 31),    # ragged rows (a 1-row tile) and columns (two x-tiles)
     (40, 512, 5),       # one K slice: outputs stored without the reduce kernel
     (3000, 2048, 32),
+    (50, 384, 20),      # 12 blocks: the second half-slice has 4 blocks (Q4_1; Q4_0 rows are not 16-B)
+    (300, 1280, 24),    # 40 blocks: the last slice has no second half
 ]
 
 
