@@ -585,8 +585,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     weight_prologue(true);
 
     if (LK_PROLOGUE_ORDER != 2) {
+#ifndef LK_NO_XWAIT  // lab: decode against whatever the image holds (wrong results): the x latency's share
       wait_vmcnt<(LK_PROLOGUE_ORDER == 0 ? G::D : G::D - 1) * G::L>();  // this wave's activation DMA has landed
       __builtin_amdgcn_s_barrier();  // ... and every other wave's
+#endif
     }
     }
 
@@ -852,6 +854,10 @@ __device__ __forceinline__ void accumulate(f32x4 &acc, float s1, float s2, f32x4
 // acc += s1·p (+ s2·T for Q4_1) as four scalar FMAs: v_pk_fma_f32 beside MFMAs costs more
 // issue time than two v_fma_f32 (MI355X_MICROARCH.md, cycle constants), and the library is
 // built with -fno-slp-vectorize so the compiler does not pack these back.
+// A SIMD issues a wave64 v_pk_fma_f32 as fast as a v_fma_f32 (tools/lab/valu_rate.hip: ~4.3-4.7
+// cycles each at one or two waves per SIMD). Measured per kernel (tools/lab/pk_ab.sh, two boxes):
+// the wide GEMM runs C5 2-3 % faster with the packed form (accumulate), the wave-pair skinny
+// kernel 1-3 % slower, so each keeps its own.
 template <bool HAS_MIN>
 __device__ __forceinline__ void accumulate_s(f32x4 &acc, float s1, float s2, f32x4 p, f32x4 t) {
   if constexpr (HAS_MIN) {
@@ -2029,7 +2035,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
             f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[bb][j]), wf[i],
                                                               f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[bb][j]), wf[i], p, 0, 0, 0);
-            accumulate_s<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], p, t);
+            accumulate<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], p, t);
           }
         }
       }
