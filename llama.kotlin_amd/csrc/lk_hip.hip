@@ -622,7 +622,6 @@ int launch_q32_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const C
 template <int QT, int NT, bool SOLO>
 int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   using SG = SkGeom<QT, NT>;
-  using SG1 = Sk1Geom<QT, NT>;
   GemmScratch &S = gemm_scratch();
   const int64_t nblk = c.K / 32, ntx = (c.N + 15) / 16;
   const size_t fb = (size_t)ntx * nblk * kXSplits * 64 * 16, sb = (size_t)nblk * ntx * 16 * sizeof(float);
@@ -657,8 +656,12 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   g.tasks = ranges * slices;
   hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
-  if (SOLO) hipLaunchKernelGGL((gemm_sk1_kernel<QT, NT>), dim3(grid), dim3(SG1::NW * 64), SG1::LDS, st, g);
-  else hipLaunchKernelGGL((gemm_sk_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
+  if constexpr (SOLO) {
+    using SG1 = Sk1Geom<QT, NT>;
+    hipLaunchKernelGGL((gemm_sk1_kernel<QT, NT>), dim3(grid), dim3(SG1::NW * 64), SG1::LDS, st, g);
+  } else {
+    hipLaunchKernelGGL((gemm_sk_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
+  }
   if (slices > 1) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
@@ -912,6 +915,13 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
       HIP_TRY(hipGetLastError());
       return LK_OK;
     }
+    // Q4_K at 16 <= N <= 32: the wave-pair MFMA kernel (lk_skinny.hpp; one Q4_K block per wave
+    // and unit, affine weights within the F32 bar); smaller batches keep the exact-decode kernels
+    // below (their weights are the Kotlin values bit for bit). LK_KQ_SK=0: lab A/B.
+    static const bool kq_sk = [] { const char *e = getenv("LK_KQ_SK"); return !e || atoi(e) != 0; }();
+    if (kq_sk && a->type == LK_TYPE_Q4_K && c.N >= 16 && c.N <= 32 && ((uintptr_t)g.a & 15) == 0 &&
+        (uint64_t)(c.K / LK_QK_K) * LK_Q4_K_BLOCK_BYTES * 16 < (1ull << 31))
+      return c.N <= 16 ? launch_sk_t<LK_TYPE_Q4_K, 1, false>(a, b, dst, c, st) : launch_sk_t<LK_TYPE_Q4_K, 2, false>(a, b, dst, c, st);
     // batch > 1: NC columns per workgroup staged in LDS (NC = 8 / 4 / 2 as K allows)
     const size_t col_lds = (size_t)(c.K / 32) * 36 * sizeof(float);
     int nc = 0;

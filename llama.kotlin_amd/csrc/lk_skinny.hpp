@@ -36,14 +36,19 @@ namespace lk {
 #define LK_SK_PRIO 1
 #endif
 
+// Bytes per 32 weights: Q4_0 18, Q4_1 20, and Q4_K 18 (a 144-byte block of 256 weights: d, dmin,
+// 12 scale bytes, 128 code bytes; core/GGMLComputeOps.kt:241-310). For Q4_K a "block" here is
+// one 32-weight sub-block (one MFMA step), and a wave's 8 blocks are exactly one Q4_K block.
+template <int QT> struct SkBB { static constexpr int v = QT == LK_TYPE_Q4_1 ? 20 : 18; };
+
 template <int QT, int NT> struct SkGeom {
   static constexpr int NW = 8;                          // 4 streams x 2 halves
-  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr int BB = SkBB<QT>::v;
   static constexpr int SB = 16, SBH = 8;                // blocks per slice / per half
   static constexpr int RPH = SBH * BB;                  // bytes of a half row piece (144 / 160)
   static constexpr int PPH = RPH / 16;                  // 16-B cells per half row
   static constexpr int L = (16 * PPH + 63) / 64;        // DMA instructions per half unit
-  static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : 3;
+  static constexpr int WPB = QT == LK_TYPE_Q4_K ? 1 : QT == LK_TYPE_Q4_1 ? 2 : 3;
   static constexpr int SLOT = L * 1024;
   static constexpr int XI = SB * NT * kXSplits;         // 1-KB activation fragments of the slice
   static constexpr int XF = XI * 1024;
@@ -107,8 +112,10 @@ __device__ __forceinline__ uint32_t lds32(const lu8 *p) { return *(const LK_LDS 
 // bg = bm + 4g (as skinny_read in lk_kernels.hpp).
 template <int QT, int B, int WPB>
 __device__ __forceinline__ void sk_read(const lu8 *bm, const lu8 *bg, uint32_t (&w)[WPB]) {
-  constexpr int OB = B * QTraits<QT>::BB;
-  if constexpr (QT == LK_TYPE_Q4_1) {  // (d, m) dword; codes at +4 + 4g
+  constexpr int OB = B * SkBB<QT>::v;
+  if constexpr (QT == LK_TYPE_Q4_K) {  // sub-block B's 16 code bytes at 16 + 16B; lane group g: 4 of them
+    w[0] = lds32(bg + 16 + 16 * B);
+  } else if constexpr (QT == LK_TYPE_Q4_1) {  // (d, m) dword; codes at +4 + 4g
     w[0] = lds32(bm + OB);
     w[1] = lds32(bg + OB + 4);
   } else if constexpr ((OB & 3) == 0) {  // d lo; codes at +2 + 4g: two dwords, realigned by 2
@@ -141,13 +148,26 @@ __device__ __forceinline__ bf16x8 q4_codes_128(uint32_t u) {
   return __builtin_bit_cast(bf16x8, w);
 }
 
+// Q4_K block header of the lane's row (per unit): h = its first 16 bytes (d, dmin, 12 scale
+// bytes), dk = d/945 (= d/63/15). Sub-block sb's weights are w = (q/15)·scale + min with
+// scale = (qs/63)·d, min = (qm/63)·d + dmin (:285-286, :298): here as the affine q·s1 + min with
+// s1 = qs·dk — the same values up to the f32 rounding of the Kotlin expression order (the
+// batch-1 kernel keeps the Kotlin order bit for bit; this MFMA path is within the F32 bar).
+struct SkHdr {
+  uint32_t h[4];
+  float dk, d63, dmin;
+};
+
 // Block B of a unit: codes + scale d from its dwords, 2·NT MFMAs into p.
 template <int QT, int NT, int B, int WPB, int NBW>
 __device__ __forceinline__ void sk_mfma(const uint32_t (&w)[WPB], const u32x4 (&xh)[NBW][NT], const u32x4 (&xl)[NBW][NT],
-                                        f32x4 (&p)[NT], float &s1) {
-  constexpr int OB = B * QTraits<QT>::BB;
+                                        f32x4 (&p)[NT], float &s1, const SkHdr &hd) {
+  constexpr int OB = B * SkBB<QT>::v;
   bf16x8 wf;
-  if constexpr (QT == LK_TYPE_Q4_1) {
+  if constexpr (QT == LK_TYPE_Q4_K) {
+    wf = q4_codes_128(w[0]);
+    s1 = (float)((hd.h[1 + B / 4] >> (8 * (B % 4))) & 0x3Fu) * hd.dk;
+  } else if constexpr (QT == LK_TYPE_Q4_1) {
     wf = q4_codes_128(w[1]);
     s1 = h2f(w[0]);
   } else if constexpr ((OB & 3) == 0) {
@@ -201,14 +221,14 @@ __device__ __forceinline__ void sk_interleave() {
 // All NBW blocks of a unit, pipelined: block B's MFMAs go out before block B − 1 is scaled in.
 template <int QT, int NT, int WPB, bool MASK, int B, int NBW>
 __device__ __forceinline__ void sk_blocks(const uint32_t (&w)[NBW][WPB], const u32x4 (&xh)[NBW][NT], const u32x4 (&xl)[NBW][NT],
-                                          int nb, f32x4 (&pp)[NT], float ps1, f32x4 (&acc)[NT]) {
+                                          int nb, f32x4 (&pp)[NT], float ps1, f32x4 (&acc)[NT], const SkHdr &hd) {
   if constexpr (B < NBW) {
     f32x4 p[NT];
     float s1;
-    sk_mfma<QT, NT, B, WPB, NBW>(w[B], xh, xl, p, s1);
+    sk_mfma<QT, NT, B, WPB, NBW>(w[B], xh, xl, p, s1, hd);
     if constexpr (B > 0) sk_scale<NT, B - 1, MASK>(pp, ps1, nb, acc);
     if constexpr (B == NBW - 1) sk_scale<NT, NBW - 1, MASK>(p, s1, nb, acc);
-    else sk_blocks<QT, NT, WPB, MASK, B + 1, NBW>(w, xh, xl, nb, p, s1, acc);
+    else sk_blocks<QT, NT, WPB, MASK, B + 1, NBW>(w, xh, xl, nb, p, s1, acc, hd);
   }
 }
 
@@ -384,35 +404,61 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 #endif
       uint32_t wd[8][G::WPB];
       uint32_t eb[2];  // the header (d, and m for Q4_1) of block 4c + (lane >> 4) of the lane's row
+      uint32_t ek[2];  // Q4_K: sub-block 4c + (lane >> 4)'s min-high byte
+      SkHdr hd{};
       {
         const lu8 *bm = ring + slot * G::SLOT + (lane & 15) * G::RPH;
         const lu8 *bg = bm + 4 * (lane >> 4);
         sk_read_all<QT, G::WPB, 0, 8>(bm, bg, wd);
+        if constexpr (QT == LK_TYPE_Q4_K) {
 #pragma unroll
-        for (int c = 0; c < 2; c++) {
-          const lu8 *hp = bm + (4 * c + (lane >> 4)) * BB;
-          if constexpr (QT == LK_TYPE_Q4_1) eb[c] = lds32(hp);
-          else eb[c] = *(const LK_LDS uint16_t *)hp;
+          for (int i = 0; i < 4; i++) hd.h[i] = lds32(bm + 4 * i);
+#pragma unroll
+          for (int c = 0; c < 2; c++) {
+            const int sbl = 4 * c + (lane >> 4);
+            eb[c] = *(const LK_LDS uint8_t *)(bm + 4 + sbl);                       // scale byte (:274)
+            ek[c] = sbl * 2 + 1 < LK_K_SCALE_SIZE ? *(const LK_LDS uint8_t *)(bm + 5 + 2 * sbl) : 0u;  // (:279-282)
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 2; c++) {
+            const lu8 *hp = bm + (4 * c + (lane >> 4)) * BB;
+            if constexpr (QT == LK_TYPE_Q4_1) eb[c] = lds32(hp);
+            else eb[c] = *(const LK_LDS uint16_t *)hp;
+          }
         }
         asm volatile("" ::: "memory");
+      }
+      if constexpr (QT == LK_TYPE_Q4_K) {
+        const float d = h2f(hd.h[0]);
+        hd.dk = d * (1.0f / 945.0f);
+        hd.d63 = d * (1.0f / 63.0f);
+        hd.dmin = h2f(hd.h[0] >> 16);
       }
       f32x4 pp[NT];
 #ifdef LK_SK_NOCOMP  // lab: the skeleton without decode / MFMAs
       acc[0].x += __builtin_bit_cast(float, wd[0][0] ^ wd[7][1]);
 #else
       if (nbh == 8) {
-        sk_blocks<QT, NT, G::WPB, false, 0, 8>(wd, xh, xl, nbh, pp, 0.f, acc);
+        sk_blocks<QT, NT, G::WPB, false, 0, 8>(wd, xh, xl, nbh, pp, 0.f, acc, hd);
         sk_interleave<8 * 2 * NT>();
       } else {
-        sk_blocks<QT, NT, G::WPB, true, 0, 8>(wd, xh, xl, nbh, pp, 0.f, acc);
+        sk_blocks<QT, NT, G::WPB, true, 0, 8>(wd, xh, xl, nbh, pp, 0.f, acc, hd);
       }
 #endif
       // the offsets: acc += Σ_b e_b·S_b over the 8 blocks (f32 MFMA, K = 4 blocks each)
 #pragma unroll
       for (int c = 0; c < 2; c++) {
         float e;
-        if constexpr (QT == LK_TYPE_Q4_1) e = fmaf(-128.f, h2f(eb[c]), h2f(eb[c] >> 16));
-        else e = -136.f * h2f(eb[c]);
+        if constexpr (QT == LK_TYPE_Q4_K) {  // min − 128·s1 of sub-block 4c + (lane >> 4)
+          const float s1 = (float)(eb[c] & 0x3Fu) * hd.dk;
+          const float mn = fmaf((float)(((eb[c] >> 6) & 3u) | ((ek[c] & 0x0Fu) << 2)), hd.d63, hd.dmin);
+          e = fmaf(-128.f, s1, mn);
+        } else if constexpr (QT == LK_TYPE_Q4_1) {
+          e = fmaf(-128.f, h2f(eb[c]), h2f(eb[c] >> 16));
+        } else {
+          e = -136.f * h2f(eb[c]);
+        }
         if (4 * c + (lane >> 4) >= nbh) e = 0.f;  // stale header bytes past the wave's blocks
 #pragma unroll
         for (int j = 0; j < NT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(sf[c][j], e, acc[j], 0, 0, 0);
@@ -462,8 +508,9 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 // banks), landed by the wave's own LDS-DMA ring. With the VALU per block at 8 + 1 + NT·2 the
 // lone wave issues its MFMAs and VALU back to back; nothing waits on a partner.
 template <int QT, int NT> struct Sk1Geom {
+  static_assert(QT != LK_TYPE_Q4_K, "Q4_K runs on the wave-pair kernel (a wave's 8 blocks = one Q4_K block)");
   static constexpr int NW = 4;
-  static constexpr int BB = QTraits<QT>::BB;
+  static constexpr int BB = SkBB<QT>::v;
   static constexpr int SB = 16;                          // blocks per slice (= per wave)
   static constexpr int RP = SB * BB;                     // row bytes of a unit (288 / 320)
   static constexpr int PPR = RP / 16;                    // 16-B cells per row
@@ -601,10 +648,10 @@ __global__ __launch_bounds__(256, 1) void gemm_sk1_kernel(SkArgs g) {
     }
     f32x4 pp[NT];
     if (nb == SB) {
-      sk_blocks<QT, NT, G::WPB, false, 0, SB>(wd, xh, xl, nb, pp, 0.f, acc);
+      sk_blocks<QT, NT, G::WPB, false, 0, SB>(wd, xh, xl, nb, pp, 0.f, acc, SkHdr{});
       sk_interleave<SB * 2 * NT>();
     } else {
-      sk_blocks<QT, NT, G::WPB, true, 0, SB>(wd, xh, xl, nb, pp, 0.f, acc);
+      sk_blocks<QT, NT, G::WPB, true, 0, SB>(wd, xh, xl, nb, pp, 0.f, acc, SkHdr{});
     }
 #pragma unroll
     for (int c = 0; c < 4; c++) {

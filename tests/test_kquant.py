@@ -11,7 +11,7 @@ import pytest
 
 import oracle as O
 from _kquant import BB, Q2_K, Q4_K, Q8_K, mat_mul_kq_ref, random_kblocks
-from _util import parity_ok, random_acts
+from _util import acc_noise, parity_ok, random_acts
 
 KQ = [Q2_K, Q4_K, Q8_K]
 KNAME = {Q2_K: "Q2_K", Q4_K: "Q4_K", Q8_K: "Q8_K"}
@@ -54,6 +54,37 @@ GPU_SHAPES = SMALL + [(257, 4096, 1), (64, 11008, 2), (100, 4096, 4), (33, 2048,
                       (40, 4096, 32), (17, 11008, 7)]
 
 
+def mfma_path(qt, K, N):
+    """Q4_K at 16 <= N <= 32 (K % 256 == 0) runs on the MFMA kernel (lk_skinny.hpp): activations
+    split as bf16 hi + lo, weights as the affine q·(scale/15) + min of the Kotlin expression."""
+    return qt == Q4_K and 16 <= N <= 32 and K % 256 == 0
+
+
+def q4k_terms(raw, M, K):
+    """|q/15·scale| + |min| per weight of a Q4_K matrix with K % 256 == 0 (numpy, the Kotlin
+    expressions of :285-298 op for op in f32): the magnitudes the affine form q·s1 + min adds."""
+    b = np.asarray(raw, np.uint8).reshape(-1, 144)
+    d = b[:, 0:2].copy().view(np.float16).astype(np.float32)[:, 0]
+    dmin = b[:, 2:4].copy().view(np.float16).astype(np.float32)[:, 0]
+    sc = b[:, 4:12].astype(np.int32)                                   # scale bytes of sub-blocks 0..7
+    mh = np.zeros_like(sc)
+    mh[:, :6] = b[:, 5:16:2][:, :6].astype(np.int32) & 0x0F          # byte 4 + 2sb + 1 < 16 for sb <= 5
+    scale = (np.float32(1) * (sc & 0x3F).astype(np.float32) / np.float32(63)) * d[:, None]
+    qm = ((sc >> 6) & 3) | (mh << 2)
+    mn = (qm.astype(np.float32) / np.float32(63)) * d[:, None] + dmin[:, None]
+    q = np.stack([b[:, 16:144] & 0x0F, b[:, 16:144] >> 4], axis=-1).reshape(-1, 8, 32).astype(np.float32)
+    t = np.abs(q / np.float32(15) * scale[:, :, None]) + np.abs(mn)[:, :, None]
+    return t.reshape(M, K)
+
+
+def kq_noise(qt, raw, M, K, x):
+    """The batched-path allowance (tests/_util.py acc_noise with the activation split) taken over
+    the affine form's term magnitudes, x4 for the f32 rounding of q·s1 + min against the Kotlin
+    expression order (a few ulps of each term)."""
+    assert qt == Q4_K
+    return 4.0 * acc_noise(q4k_terms(raw, M, K), np.abs(x), split=True)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("qt", KQ, ids=lambda t: KNAME[t])
 @pytest.mark.parametrize("shape", GPU_SHAPES, ids=lambda s: "x".join(map(str, s)))
@@ -63,12 +94,33 @@ def test_kquant_gpu_vs_oracle(gpu, qt, shape):
     raw = random_kblocks(qt, M * K // 256, seed=M + K + N)
     x = _x(K, N, 11 + N)
     ref = O.mat_mul_q(qt, raw, M, K, x)
+    noise = kq_noise(qt, raw, M, K, x) if mfma_path(qt, K, N) else None
     got = gpu_matmul(qt, raw, M, K, N, x)
-    ok, msg = parity_ok(got, ref)
+    ok, msg = parity_ok(got, ref, noise=noise)
     assert ok, msg
     got = gpu_matmul(qt, raw, M, K, N, x, host=True, dst_row_pad=2)
-    ok, msg = parity_ok(got, ref)
+    ok, msg = parity_ok(got, ref, noise=noise)
     assert ok, ("host path", msg)
+
+
+# The Q4_K MFMA path (16 <= N <= 32): ragged rows, K with a half slice at the end (11008 = 43
+# blocks: the last slice's second half is empty), one 16-column tile, and bit-equal reruns.
+KQ_MFMA = [(257, 4096, 32), (100, 11008, 17), (33, 2048, 16), (1000, 1024, 24), (64, 256, 20)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", KQ_MFMA, ids=lambda s: "x".join(map(str, s)))
+def test_q4_k_mfma_vs_oracle(gpu, shape):
+    from test_gpu_parity import gpu_matmul
+    M, K, N = shape
+    raw = random_kblocks(Q4_K, M * K // 256, seed=7 * M + N)
+    x = _x(K, N, 31 + N)
+    ref = O.mat_mul_q(Q4_K, raw, M, K, x)
+    got = gpu_matmul(Q4_K, raw, M, K, N, x)
+    ok, msg = parity_ok(got, ref, noise=kq_noise(Q4_K, raw, M, K, x))
+    assert ok, msg
+    again = gpu_matmul(Q4_K, raw, M, K, N, x)
+    assert np.array_equal(got.view(np.uint32), again.view(np.uint32)), "not deterministic"
 
 
 @pytest.mark.gpu
