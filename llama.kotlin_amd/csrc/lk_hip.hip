@@ -654,7 +654,12 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
     g.partial = (float *)S.partial;
   }
   g.tasks = ranges * slices;
-  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  // dense, 16-B aligned B (every Llama activation): the GEMM splits its slice itself (no xsplit
+  // launch); LK_SK_XSPLIT=1 forces the separate split (lab A/B)
+  static const bool force_xsplit = getenv("LK_SK_XSPLIT") != nullptr;
+  g.b = xa.b;
+  g.fx = !SOLO && !force_xsplit && b->nb[0] == 4 && b->nb[1] == 4 * (uint64_t)c.N && ((uintptr_t)xa.b & 15) == 0;
+  if (!g.fx) hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   if constexpr (SOLO) {
     using SG1 = Sk1Geom<QT, NT>;

@@ -69,8 +69,10 @@ template <int QT, int NT> struct SkGeom {
 
 struct SkArgs {
   const uint8_t *a;        // weights (buffer base + dataOffset), rows RB bytes apart
-  const u32x4 *frag;       // xsplit_kernel fragments [ntx][nblk][2][64]
-  const float *xsum;       // [nblk][16·ntx]: Σx per (block, column) (Q4_1)
+  const u32x4 *frag;       // xsplit_kernel fragments [ntx][nblk][2][64] (fx == 0)
+  const float *xsum;       // [nblk][16·ntx]: Σ(hi + lo) per (block, column) (fx == 0)
+  const uint8_t *b;        // fx == 1: dense B (k-major rows of N floats, 16-B aligned), split in-kernel
+  int32_t fx;
   uint8_t *dst;            // dst(n, m) at n·d_nb0 + m·d_nb1
   int64_t d_nb0, d_nb1;
   float *partial;          // [slices][M][16·NT] when slices > 1
@@ -305,12 +307,20 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   // 1. the first weight unit; the slice's activation fragments (and Q4_1 block sums) into LDS,
   //    spread over the workgroup's waves; the rest of the ring
   if (myL && nunits > 0) issue(0, 0);
-  for (int i = wave; i < G::XI; i += G::NW) {  // fragment i: tile i / 32, block (i % 32) / 2, split i % 2
-    const int j = i / (2 * G::SB), b = (i % (2 * G::SB)) / 2, sp = i % 2;
-    const int kb = b < nb ? kb0 + b : kb0;      // past a short slice: any valid fragment (masked)
-    dma16l<false>(g.frag, (uint32_t)((((int64_t)j * nblk + kb) * kXSplits + sp) * 1024 + lane * 16), xlds + i * 1024);
-  }
-  {
+  const int rbytes = 128 * nb * g.N;  // fx: the slice's raw activations, k-major rows of N floats
+  if (g.fx) {
+    const uint8_t *src = g.b + (int64_t)kb0 * 128 * g.N;
+    for (int q = wave; q * 1024 < rbytes; q += G::NW) {
+      int off = q * 1024 + lane * 16;
+      off = off < rbytes ? off : rbytes - 16;   // lanes past the slice re-read its last piece (unused)
+      dma16l<false>(src, (uint32_t)off, xlds + q * 1024);
+    }
+  } else {
+    for (int i = wave; i < G::XI; i += G::NW) {  // fragment i: tile i / 32, block (i % 32) / 2, split i % 2
+      const int j = i / (2 * G::SB), b = (i % (2 * G::SB)) / 2, sp = i % 2;
+      const int kb = b < nb ? kb0 + b : kb0;      // past a short slice: any valid fragment (masked)
+      dma16l<false>(g.frag, (uint32_t)((((int64_t)j * nblk + kb) * kXSplits + sp) * 1024 + lane * 16), xlds + i * 1024);
+    }
     const int n16 = 16 * NT;
     const int64_t tot = (int64_t)nblk * n16;   // floats in xsum
     if (wave < G::TI) {
@@ -321,11 +331,63 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   }
   if (myL)
     for (int u = 1; u < min(D, nunits); u++) issue(u, u);
-  // fragments landed (and this wave's unit 0: the DMA before them), flags written; the ring's
-  // later units stay in flight across the bare barrier
+  // x landed (and this wave's unit 0: the DMA before it), flags written; the ring's later units
+  // stay in flight across the bare barriers
   wait_vmcnt_rt<G::MAXW>(myL * max(0, min(D - 1, nunits - 1)));
   wait_lgkmcnt0();
   __builtin_amdgcn_s_barrier();
+  if (g.fx) {
+    // split the raw slice in place into the MFMA fragments (as xsplit_kernel, q4_order 2):
+    // item (tile j, block b) -> lane (i, gq) holds x(n = 16j + i, k = 32b + 8gq + kk(e)),
+    // kk(e) = (e >> 1) + 4(e & 1); every wave reads its items, then all write
+    constexpr int NI = (16 * NT + G::NW - 1) / G::NW;  // items per wave
+    float v[NI][8];
+    const int i16 = lane & 15, gq = lane >> 4;
+#pragma unroll
+    for (int it = 0; it < NI; it++) {
+      const int item = wave + it * G::NW, j = item / 16, b = item % 16;
+      const int n = 16 * j + i16;
+      const bool ok = item < 16 * NT && b < nb && n < g.N;
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const int kl = 32 * b + 8 * gq + (e >> 1) + 4 * (e & 1);
+        v[it][e] = ok ? *(const LK_LDS float *)(xlds + (kl * g.N + n) * 4) : 0.f;
+      }
+    }
+    wait_lgkmcnt0();
+    __builtin_amdgcn_s_barrier();  // every raw value is in registers: the image may be overwritten
+#pragma unroll
+    for (int it = 0; it < NI; it++) {
+      const int item = wave + it * G::NW, j = item / 16, b = item % 16;
+      if (item >= 16 * NT) continue;
+      uint32_t hi[4], lo[4];
+      float hsum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        uint32_t hh[2], ll[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          const uint32_t bx = __builtin_bit_cast(uint32_t, v[it][e + q]);
+          const float r = v[it][e + q] - __builtin_bit_cast(float, bx & 0xFFFF0000u);  // exact
+          uint32_t br = __builtin_bit_cast(uint32_t, r);
+          br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even
+          hh[q] = bx;
+          ll[q] = br;
+          hsum += __builtin_bit_cast(float, bx & 0xFFFF0000u) + __builtin_bit_cast(float, br & 0xFFFF0000u);
+        }
+        hi[e / 2] = __builtin_amdgcn_perm(hh[1], hh[0], 0x07060302u);
+        lo[e / 2] = __builtin_amdgcn_perm(ll[1], ll[0], 0x07060302u);
+      }
+      LK_LDS u32x4 *xf = (LK_LDS u32x4 *)(xlds + ((j * G::SB + b) * kXSplits) * 1024) + lane;
+      xf[0] = u32x4{hi[0], hi[1], hi[2], hi[3]};
+      xf[64] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+      hsum += __shfl_xor(hsum, 16, kWave);
+      hsum += __shfl_xor(hsum, 32, kWave);
+      if (gq == 0) tlds[b * 16 * NT + 16 * j + i16] = hsum;
+    }
+    wait_lgkmcnt0();
+    __builtin_amdgcn_s_barrier();
+  }
   u32x4 xh[8][NT], xl[8][NT];
 #pragma unroll
   for (int b = 0; b < 8; b++)
