@@ -25,6 +25,7 @@
 #include "lk_kernels.hpp"
 #include "lk_mfma32.hpp"
 #include "lk_skinny.hpp"
+#include "lk_wide2.hpp"
 #include "../../include/lk_gguf.h"
 
 using namespace lk;
@@ -763,7 +764,10 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
   const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
   hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
-  hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
+  // LK_WIDE2=1: gemm_wide2_kernel (lk_wide2.hpp, dedicated loader waves) on the same tiles
+  static const int w2 = [] { const char *e = getenv("LK_WIDE2"); return e ? atoi(e) : 0; }();
+  if (w2) hipLaunchKernelGGL((gemm_wide2_kernel<QT>), dim3(grid), dim3(512), Wide2Geom<QT>::LDS, st, g);
+  else hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
   if (slices > 1) {
     const int64_t threads = (int64_t)g.M * (npad / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,

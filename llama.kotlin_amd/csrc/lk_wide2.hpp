@@ -1,0 +1,262 @@
+// lk_wide2.hpp — batched quantized GEMM for N > 32 (config C5's prefill) with dedicated loader waves.
+//
+// Same tiles, operands and arithmetic as gemm_wide_kernel (lk_kernels.hpp: 256-row x 64-column
+// workgroup tile, K in stages of 4 blocks through an LDS ring of D stages, bf16 hi/lo activation
+// fragments from xsplit_kernel, two v_mfma_f32_16x16x32_bf16 per block and 16x16 tile, the block
+// scale applied in f32 after the MFMA). What changes is who waits for whom. gemm_wide_kernel has
+// every wave issue its share of a stage's DMA and meets the others at two workgroup barriers per
+// stage, so the DMA, the LDS reads and the MFMAs of the workgroup run one after the other (its
+// lab skeleton: DMA + barriers alone 21 µs, + LDS reads 35, + compute 51-55 µs per C5 call).
+// Here the 8 waves split by role, one of each per SIMD:
+//   * waves 0-3, consumers: wave c owns rows [64c, 64c + 64) of the tile and all 64 columns over
+//     the whole K slice (4 x 4 MFMA tiles, no K-group reduction); per stage it waits until the
+//     stage's slot is FULL, reads each block's operands from LDS and computes, and marks the slot
+//     FREE once its last LDS read of the stage has landed;
+//   * waves 4-7, loaders: each issues a fixed quarter of every stage's LDS-DMA instructions,
+//     marks the stage FULL once its own pieces have landed (vmcnt), and refills a slot once the
+//     four consumers have freed it — up to D - 1 stages ahead of the slowest consumer.
+// FULL / FREE are monotonic per-slot LDS counters (4 arrivals per use), so no wave waits at a
+// workgroup barrier after the prologue and the DMA stream overlaps the MFMAs.
+#pragma once
+
+#include "lk_kernels.hpp"
+#include "lk_skinny.hpp"
+
+namespace lk {
+
+template <int QT> struct Wide2Geom {
+  using W = WideGeom<QT>;
+  static constexpr int NC = 4, NL = 4;                          // consumer / loader waves
+  static constexpr int MT = 4, NT = 4, BM = NC * MT * 16, BN = NT * 16;
+  static constexpr int TOT = W::W_INST + W::X_INST + W::T_INST;  // DMA instructions per stage
+  static constexpr int CWL = (TOT + NL - 1) / NL;               // per loader (dummies pad the last)
+  static constexpr int STAGE = W::STAGE;
+  static constexpr int CNT = 64;                                // FULL[D], FREE[D] (ints)
+  static constexpr int D = ((kLdsBytes - CNT) / STAGE) > 4 ? 4 : ((kLdsBytes - CNT) / STAGE);
+  static constexpr int LDS = D * STAGE + CNT;
+  static_assert(BM == W::BM && BN == W::BN, "same tile as gemm_wide_kernel");
+  static_assert(D >= 2, "ring");
+  static_assert(D * CWL < 64, "vmcnt");
+};
+
+template <int QT>
+__global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
+  using G = Wide2Geom<QT>;
+  using WG = WideGeom<QT>;
+  constexpr int MT = G::MT, NT = G::NT, BM = G::BM, BN = G::BN, BB = WG::BB, SB = WG::SB, D = G::D;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  lu8 *const sbase = (lu8 *)smem;
+  LK_LDS int *full = (LK_LDS int *)(sbase + D * G::STAGE);
+  LK_LDS int *freec = full + 8;
+  // task order as gemm_wide_kernel (XCD super-tiles; speed only)
+  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+  if (task >= g.tasks) return;
+  const int slice = task % g.slices, u = task / g.slices;
+  const int per_st = g.sm * g.sn, nsn = (g.tiles_n + g.sn - 1) / g.sn;
+  const int st_idx = u / per_st, within = u % per_st;
+  const int tm = (st_idx / nsn) * g.sm + within / g.sn, tn = (st_idx % nsn) * g.sn + within % g.sn;
+  if (tm >= g.tiles_m || tn >= g.tiles_n) return;  // the whole workgroup leaves (before the barrier)
+  const int nblk = g.K / 32;
+  const int kb0 = slice * g.kslice, kb1 = min(kb0 + g.kslice, nblk);
+  const int nst = (kb1 - kb0) / SB;
+  const int64_t RB = (int64_t)nblk * BB;
+  const int ntx = (g.N + 15) / 16, n16 = ntx * 16;
+  if (threadIdx.x < 16) full[threadIdx.x] = 0;
+  wait_lgkmcnt0();
+  __builtin_amdgcn_s_barrier();
+  if (nst <= 0) return;
+
+  if (wave >= G::NC) {
+    // ---- loader ----
+    const int lw = wave - G::NC;
+    uint32_t ofs[G::CWL];
+    int kind[G::CWL];  // 0 weights, 1 activations, 2 Σx, 3 padding
+    uint32_t dsto[G::CWL];
+#pragma unroll
+    for (int c = 0; c < G::CWL; c++) {
+      const int q = lw + G::NL * c;
+      if (q < WG::W_INST) {
+        const int piece = min(q * 64 + lane, WG::WPIECES - 1);
+        const int r = piece / (WG::WIN / 16), pc = piece % (WG::WIN / 16);
+        const int64_t row = min((int64_t)tm * BM + r, (int64_t)g.M - 1);
+        ofs[c] = (uint32_t)(row * RB + pc * 16);
+        kind[c] = 0;
+        dsto[c] = q * 1024;
+      } else if (q < WG::W_INST + WG::X_INST) {
+        const int x = q - WG::W_INST;  // (block b, x-tile j, split s)
+        const int b = x / (NT * kXSplits), j = (x / kXSplits) % NT, sp = x % kXSplits;
+        const int xt = min(tn * NT + j, ntx - 1);
+        ofs[c] = (uint32_t)((((int64_t)xt * nblk + b) * kXSplits + sp) * 1024 + lane * 16);
+        kind[c] = 1;
+        dsto[c] = WG::W_BYTES + x * 1024;
+      } else if (q < G::TOT) {  // Q4_1: the stage's Σx, lane -> (block, 4 columns)
+        const int li = min(lane, SB * BN / 4 - 1);
+        const int b = li / (BN / 4), c4 = li % (BN / 4);
+        const int n = min(tn * BN + 4 * c4, n16 - 4);
+        ofs[c] = (uint32_t)(((int64_t)b * n16 + n) * 4);
+        kind[c] = 2;
+        dsto[c] = WG::T_OFF;
+      } else {
+        ofs[c] = 0;
+        kind[c] = 3;
+        dsto[c] = WG::DUMMY;
+      }
+    }
+    auto issue = [&](int st) __attribute__((always_inline)) {
+      const int kb = kb0 + st * SB;
+      lu8 *slot = sbase + (st % D) * G::STAGE;
+#pragma unroll
+      for (int c = 0; c < G::CWL; c++) {
+        const uint8_t *base = kind[c] == 1 ? (const uint8_t *)g.frag + (int64_t)kb * kXSplits * 1024
+                              : kind[c] == 2 ? (const uint8_t *)(g.xsum + (int64_t)kb * n16)
+                                             : g.a + (int64_t)kb * BB;
+        dma16l<false>(base, ofs[c], slot + dsto[c]);
+      }
+    };
+    const int pro = min(D, nst);
+    for (int s = 0; s < pro; s++) issue(s);
+    for (int s = 0; s < nst; s++) {
+      // stage s landed: the younger ones in flight are stages s+1 .. s+D-1 (prologue) / s+D-2
+      const int hi = min(nst - 1, s == 0 ? pro - 1 : s + D - 2);
+      wait_vmcnt_rt<(D - 1) * G::CWL>(G::CWL * (hi - s));
+      if (lane == 0) __hip_atomic_fetch_add(full + s % D, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // refill the slot of stage s - 1 once the consumers are done with it
+      if (s >= 1 && s - 1 + D < nst) {
+        const int need = G::NC * ((s - 1) / D + 1);
+        while (ldsl_ld(freec + (s - 1) % D) < need) __builtin_amdgcn_s_sleep(1);
+        issue(s - 1 + D);
+      }
+    }
+    return;
+  }
+
+  // ---- consumer ----
+  // One block of lookahead: block gb + 1's operands are read from LDS while block gb's MFMAs run
+  // (a stage's slot is freed once its last block's reads have landed).
+  const int mw = wave;
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int m = lane & 15, gq = lane >> 4;
+  constexpr int WD = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
+  struct Ops {
+    uint32_t wd[MT][WD];
+    u32x4 xh[NT], xl[NT];
+    f32x4 tq[NT];
+  };
+  auto load = [&](int gb, Ops &o) __attribute__((always_inline)) {
+    const int s = gb / SB, b = gb % SB, sl = s % D;
+    const lu8 *W = sbase + sl * G::STAGE;
+    const lu8 *X = W + WG::W_BYTES;
+    const int ob = b * BB;
+#pragma unroll
+    for (int i = 0; i < MT; i++) {
+      const lu8 *rowp = W + ((mw * MT + i) * 16 + m) * WG::WIN;
+      if constexpr (QT == LK_TYPE_Q4_1) {
+        o.wd[i][0] = lds32(rowp + ob);
+        o.wd[i][1] = lds32(rowp + ob + 4 + 4 * gq);
+      } else if constexpr (QT == LK_TYPE_Q4_0) {  // 18-B blocks: even b 4-aligned
+        const int e = (b & 1) ? -2 : 0;             // odd b: d in the high half of the dword before
+        o.wd[i][0] = lds32(rowp + ob + e);
+        o.wd[i][1] = lds32(rowp + ob + 4 * gq - e);
+        o.wd[i][2] = lds32(rowp + ob + 4 * gq + 4);
+      } else {
+        const int e = (b & 1) ? -2 : 0;
+        o.wd[i][0] = lds32(rowp + ob + e);
+        o.wd[i][1] = lds32(rowp + ob + 8 * gq - e);
+        o.wd[i][2] = lds32(rowp + ob + 8 * gq + 4 - e);
+        o.wd[i][3] = lds32(rowp + ob + 8 * gq + 8);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const LK_LDS u32x4 *xf = (const LK_LDS u32x4 *)(X + ((b * NT + j) * kXSplits) * 1024) + lane;
+      o.xh[j] = xf[0];
+      o.xl[j] = xf[64];
+    }
+    if constexpr (QT == LK_TYPE_Q4_1) {
+      const LK_LDS float *T = (const LK_LDS float *)(W + WG::T_OFF);
+#pragma unroll
+      for (int j = 0; j < NT; j++) o.tq[j] = *(const LK_LDS f32x4 *)(T + b * BN + j * 16 + gq * 4);
+    }
+  };
+  auto compute = [&](int gb, const Ops &o) __attribute__((always_inline)) {
+    const bool odd = (gb % SB) & 1;
+    bf16x8 wf[MT];
+    float s1[MT], s2[MT];
+#pragma unroll
+    for (int i = 0; i < MT; i++) {
+      s2[i] = 0.f;
+      if constexpr (QT == LK_TYPE_Q4_1) {
+        wf[i] = Q4Frag<0>::make(o.wd[i][1]);
+        s1[i] = 512.f * h2f(o.wd[i][0]);
+        s2[i] = h2f(o.wd[i][0] >> 16);
+      } else if constexpr (QT == LK_TYPE_Q4_0) {  // even: codes straddle (realign); odd: aligned
+        wf[i] = q4_0_frag_biased(odd ? o.wd[i][1] : align2(o.wd[i][2], o.wd[i][1]));
+        s1[i] = 512.f * h2f(odd ? o.wd[i][0] >> 16 : o.wd[i][0]);
+      } else {
+        wf[i] = odd ? w_frag<LK_TYPE_Q8_0>(o.wd[i][1], o.wd[i][2])
+                    : w_frag<LK_TYPE_Q8_0>(align2(o.wd[i][2], o.wd[i][1]), align2(o.wd[i][3], o.wd[i][2]));
+        s1[i] = h2f(odd ? o.wd[i][0] >> 16 : o.wd[i][0]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      f32x4 t = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (QT == LK_TYPE_Q4_1) t = o.tq[j];
+#pragma unroll
+      for (int i = 0; i < MT; i++) {
+        f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, o.xl[j]), wf[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, o.xh[j]), wf[i], p, 0, 0, 0);
+        accumulate<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], p, t);
+      }
+    }
+  };
+  const int nbt = nst * SB;  // blocks of the K slice
+  Ops cur, nxt;
+  while (ldsl_ld(full) < G::NC) __builtin_amdgcn_s_sleep(1);
+  load(0, cur);
+  for (int gb = 0; gb < nbt; gb++) {
+    wait_lgkmcnt0();  // block gb's operands are in registers
+    if (gb % SB == SB - 1 && lane == 0)  // the stage's last reads: the loaders may refill the slot
+      __hip_atomic_fetch_add(freec + (gb / SB) % D, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (gb + 1 < nbt) {
+      if ((gb + 1) % SB == 0) {  // the next block opens a stage: wait until it is FULL
+        const int s = (gb + 1) / SB;
+        while (ldsl_ld(full + s % D) < G::NC * (s / D + 1)) __builtin_amdgcn_s_sleep(1);
+      }
+      load(gb + 1, nxt);
+    }
+    compute(gb, cur);
+    cur = nxt;
+  }
+  // outputs: lane holds C'(n = 16·(tn·NT + j) + 4(lane>>4) + e, m = tm·BM + (mw·MT + i)·16 + (lane&15))
+  const int npad = g.tiles_n * BN;
+#pragma unroll
+  for (int i = 0; i < MT; i++) {
+    const int64_t mr = (int64_t)tm * BM + (mw * MT + i) * 16 + (lane & 15);
+    if (mr >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int n0 = tn * BN + j * 16 + 4 * (lane >> 4);
+      if (g.slices > 1) {
+        *(f32x4 *)(g.partial + (((int64_t)slice * g.M + mr) * npad + n0)) = acc[i][j];
+      } else {
+        const float e4[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
+        if (g.d_nb0 == 4 && n0 + 4 <= g.N && ((((uintptr_t)g.dst + mr * g.d_nb1 + n0 * 4) & 15) == 0)) {
+          *(f32x4 *)(g.dst + mr * g.d_nb1 + n0 * 4) = acc[i][j];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (n0 + q < g.N) *(float *)(g.dst + mr * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+        }
+      }
+    }
+  }
+}
+
+}  // namespace lk
