@@ -762,10 +762,16 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
   const int nsuper = ((g.tiles_m + g.sm - 1) / g.sm) * ((g.tiles_n + g.sn - 1) / g.sn);
   g.tasks = nsuper * g.sm * g.sn * slices;
   const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
-  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
-  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
-  // LK_WIDE2=1: gemm_wide2_kernel (lk_wide2.hpp, dedicated loader waves) on the same tiles
+  // LK_WIDE2=1: gemm_wide2_kernel (lk_wide2.hpp, dedicated loader waves) on the same tiles; its
+  // Q4 codes are 128 + n, so the activations come in xsplit's q4_order 2 with T = MULT·Σ(hi + lo)
   static const int w2 = [] { const char *e = getenv("LK_WIDE2"); return e ? atoi(e) : 0; }();
+  XSplitArgs xw = xa;
+  if (w2 && QT != LK_TYPE_Q8_0) {
+    xw.q4_order = 2;
+    xw.mult = Wide2Geom<QT>::MULT;
+  }
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xw);
+  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   if (w2) hipLaunchKernelGGL((gemm_wide2_kernel<QT>), dim3(grid), dim3(512), Wide2Geom<QT>::LDS, st, g);
   else hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
   if (slices > 1) {

@@ -24,20 +24,40 @@
 
 namespace lk {
 
+// Operands (gemm_wide2_kernel): Q4_0 / Q4_1 codes as the exact bf16 128 + n, two per v_and_or_b32
+// (lk_skinny.hpp q4_codes_128; activations in the matching k order, xsplit_kernel q4_order 2), the
+// offset entering through the first MFMA's C input: C = T = −136·S (Q4_0, xsplit mult −136) or
+// C = −128·T with T = S (Q4_1, plus m·T after the MFMA), S = Σ(hi + lo) per (block, column). The
+// stage carries T for both types; Q8_0 keeps gemm_wide_kernel's decode and has no T.
+#ifndef LK_W2_SCHED
+#define LK_W2_SCHED 1
+#endif
+
 template <int QT> struct Wide2Geom {
   using W = WideGeom<QT>;
   static constexpr int NC = 4, NL = 4;                          // consumer / loader waves
   static constexpr int MT = 4, NT = 4, BM = NC * MT * 16, BN = NT * 16;
-  static constexpr int TOT = W::W_INST + W::X_INST + W::T_INST;  // DMA instructions per stage
-  static constexpr int CWL = (TOT + NL - 1) / NL;               // per loader (dummies pad the last)
-  static constexpr int STAGE = W::STAGE;
-  static constexpr int CNT = 64;                                // FULL[D], FREE[D] (ints)
+  static constexpr bool HAS_T = QT != LK_TYPE_Q8_0;
+  static constexpr int W_BYTES = W::W_BYTES, X_BYTES = W::X_BYTES;
+  static constexpr int T_OFF = W_BYTES + X_BYTES;
+  static constexpr int STAGE = T_OFF + (HAS_T ? 1024 : 0);      // padding DMA re-issues a real piece
+  static constexpr int TOT = W::W_INST + W::X_INST + (HAS_T ? 1 : 0);  // DMA instructions per stage
+  static constexpr int CWL = (TOT + NL - 1) / NL;               // per loader
+  static constexpr int CNT = 64;                                // FULL[8], FREE[8] (ints)
   static constexpr int D = ((kLdsBytes - CNT) / STAGE) > 4 ? 4 : ((kLdsBytes - CNT) / STAGE);
   static constexpr int LDS = D * STAGE + CNT;
+  static constexpr float MULT = QT == LK_TYPE_Q4_0 ? -136.f : 1.f;  // xsplit's T = MULT·S
   static_assert(BM == W::BM && BN == W::BN, "same tile as gemm_wide_kernel");
-  static_assert(D >= 2, "ring");
+  static_assert(D >= 2 && D <= 8, "ring");
   static_assert(D * CWL < 64, "vmcnt");
+  static_assert(W::SB * BN * 4 <= 1024, "T");
 };
+
+// Lab (tools/lab/w2_trace.hip defines LK_W2_TRACE): per wave, s_memtime cycles spent waiting on
+// the FULL / FREE counters and in total.
+#ifdef LK_W2_TRACE
+__device__ uint64_t *lk_w2trace_buf;
+#endif
 
 template <int QT>
 __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
@@ -48,7 +68,7 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   lu8 *const sbase = (lu8 *)smem;
-  LK_LDS int *full = (LK_LDS int *)(sbase + D * G::STAGE);
+  LK_LDS int *full = (LK_LDS int *)(sbase + D * G::STAGE);  // (D <= 8)
   LK_LDS int *freec = full + 8;
   // task order as gemm_wide_kernel (XCD super-tiles; speed only)
   const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
@@ -68,11 +88,22 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
   __builtin_amdgcn_s_barrier();
   if (nst <= 0) return;
 
+#ifdef LK_W2_TRACE
+  uint64_t c_wait = 0;
+  const uint64_t c_start = __builtin_amdgcn_s_memtime();
+  auto trace_out = [&]() {
+    uint64_t *tb = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_w2trace_buf)[0];
+    if (lane == 0 && tb) {
+      tb[((size_t)blockIdx.x * 8 + wave) * 2 + 0] = c_wait;
+      tb[((size_t)blockIdx.x * 8 + wave) * 2 + 1] = __builtin_amdgcn_s_memtime() - c_start;
+    }
+  };
+#endif
   if (wave >= G::NC) {
     // ---- loader ----
     const int lw = wave - G::NC;
     uint32_t ofs[G::CWL];
-    int kind[G::CWL];  // 0 weights, 1 activations, 2 Σx, 3 padding
+    int kind[G::CWL];  // 0 weights, 1 activations, 2 T
     uint32_t dsto[G::CWL];
 #pragma unroll
     for (int c = 0; c < G::CWL; c++) {
@@ -91,17 +122,17 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
         ofs[c] = (uint32_t)((((int64_t)xt * nblk + b) * kXSplits + sp) * 1024 + lane * 16);
         kind[c] = 1;
         dsto[c] = WG::W_BYTES + x * 1024;
-      } else if (q < G::TOT) {  // Q4_1: the stage's Σx, lane -> (block, 4 columns)
+      } else if (G::HAS_T && q < G::TOT) {  // the stage's T, lane -> (block, 4 columns)
         const int li = min(lane, SB * BN / 4 - 1);
         const int b = li / (BN / 4), c4 = li % (BN / 4);
         const int n = min(tn * BN + 4 * c4, n16 - 4);
         ofs[c] = (uint32_t)(((int64_t)b * n16 + n) * 4);
         kind[c] = 2;
-        dsto[c] = WG::T_OFF;
-      } else {
-        ofs[c] = 0;
-        kind[c] = 3;
-        dsto[c] = WG::DUMMY;
+        dsto[c] = G::T_OFF;
+      } else {  // padding: the loader's first piece again (same bytes to the same place)
+        ofs[c] = ofs[0];
+        kind[c] = kind[0];
+        dsto[c] = dsto[0];
       }
     }
     auto issue = [&](int st) __attribute__((always_inline)) {
@@ -125,10 +156,19 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
       // refill the slot of stage s - 1 once the consumers are done with it
       if (s >= 1 && s - 1 + D < nst) {
         const int need = G::NC * ((s - 1) / D + 1);
+#ifdef LK_W2_TRACE
+        const uint64_t w0 = __builtin_amdgcn_s_memtime();
+#endif
         while (ldsl_ld(freec + (s - 1) % D) < need) __builtin_amdgcn_s_sleep(1);
+#ifdef LK_W2_TRACE
+        c_wait += __builtin_amdgcn_s_memtime() - w0;
+#endif
         issue(s - 1 + D);
       }
     }
+#ifdef LK_W2_TRACE
+    trace_out();
+#endif
     return;
   }
 
@@ -178,8 +218,8 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
       o.xh[j] = xf[0];
       o.xl[j] = xf[64];
     }
-    if constexpr (QT == LK_TYPE_Q4_1) {
-      const LK_LDS float *T = (const LK_LDS float *)(W + WG::T_OFF);
+    if constexpr (G::HAS_T) {
+      const LK_LDS float *T = (const LK_LDS float *)(W + G::T_OFF);
 #pragma unroll
       for (int j = 0; j < NT; j++) o.tq[j] = *(const LK_LDS f32x4 *)(T + b * BN + j * 16 + gq * 4);
     }
@@ -192,48 +232,88 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
     for (int i = 0; i < MT; i++) {
       s2[i] = 0.f;
       if constexpr (QT == LK_TYPE_Q4_1) {
-        wf[i] = Q4Frag<0>::make(o.wd[i][1]);
-        s1[i] = 512.f * h2f(o.wd[i][0]);
+        wf[i] = q4_codes_128(o.wd[i][1]);
+        s1[i] = h2f(o.wd[i][0]);
         s2[i] = h2f(o.wd[i][0] >> 16);
       } else if constexpr (QT == LK_TYPE_Q4_0) {  // even: codes straddle (realign); odd: aligned
-        wf[i] = q4_0_frag_biased(odd ? o.wd[i][1] : align2(o.wd[i][2], o.wd[i][1]));
-        s1[i] = 512.f * h2f(odd ? o.wd[i][0] >> 16 : o.wd[i][0]);
+        wf[i] = q4_codes_128(odd ? o.wd[i][1] : align2(o.wd[i][2], o.wd[i][1]));
+        s1[i] = h2f(odd ? o.wd[i][0] >> 16 : o.wd[i][0]);
       } else {
         wf[i] = odd ? w_frag<LK_TYPE_Q8_0>(o.wd[i][1], o.wd[i][2])
                     : w_frag<LK_TYPE_Q8_0>(align2(o.wd[i][2], o.wd[i][1]), align2(o.wd[i][3], o.wd[i][2]));
         s1[i] = h2f(odd ? o.wd[i][0] >> 16 : o.wd[i][0]);
       }
     }
+    f32x4 c0[NT], t[NT];
 #pragma unroll
     for (int j = 0; j < NT; j++) {
-      f32x4 t = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (QT == LK_TYPE_Q4_1) t = o.tq[j];
+      c0[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      t[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (QT == LK_TYPE_Q4_0) c0[j] = o.tq[j];  // −136·S
+      if constexpr (QT == LK_TYPE_Q4_1) {
+        t[j] = o.tq[j];  // S
+        const f2v k = {-128.f, -128.f};
+        const f2v a = k * f2v{t[j].x, t[j].y}, bq = k * f2v{t[j].z, t[j].w};
+        c0[j] = f32x4{a.x, a.y, bq.x, bq.y};
+      }
+    }
+    // 16 tiles, each an MFMA pair; a tile's result is scaled into acc LAG tiles later, so the
+    // VALU never waits on the MFMA it follows (one in-order wave per SIMD)
+    constexpr int NTL = MT * NT, LAG = 3;
+    f32x4 pr[LAG + 1];
 #pragma unroll
-      for (int i = 0; i < MT; i++) {
-        f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, o.xl[j]), wf[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, o.xh[j]), wf[i], p, 0, 0, 0);
-        accumulate<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], p, t);
+    for (int k = 0; k < NTL + LAG; k++) {
+      if (k < NTL) {
+        const int i = k % MT, j = k / MT;
+        f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, o.xl[j]), wf[i], c0[j], 0, 0, 0);
+        pr[k % (LAG + 1)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, o.xh[j]), wf[i], p, 0, 0, 0);
+      }
+      if (k >= LAG) {
+        const int kk = k - LAG, i = kk % MT, j = kk / MT;
+        accumulate<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], pr[kk % (LAG + 1)], t[j]);
       }
     }
   };
-  const int nbt = nst * SB;  // blocks of the K slice
-  Ops cur, nxt;
-  while (ldsl_ld(full) < G::NC) __builtin_amdgcn_s_sleep(1);
-  load(0, cur);
-  for (int gb = 0; gb < nbt; gb++) {
-    wait_lgkmcnt0();  // block gb's operands are in registers
+  const int nbt = nst * SB;  // blocks of the K slice (even: SB = 4)
+  // step gb: block gb's operands (in `use`) have landed; free its stage if it was the stage's last
+  // block, start reading block gb + 1 into `into`, then compute gb. Two buffers in ping-pong (no
+  // register copies); the MFMAs are interleaved with the decode / scale VALU.
+  auto step = [&](int gb, const Ops &use, Ops &into) __attribute__((always_inline)) {
+    wait_lgkmcnt0();
     if (gb % SB == SB - 1 && lane == 0)  // the stage's last reads: the loaders may refill the slot
       __hip_atomic_fetch_add(freec + (gb / SB) % D, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (gb + 1 < nbt) {
       if ((gb + 1) % SB == 0) {  // the next block opens a stage: wait until it is FULL
         const int s = (gb + 1) / SB;
+#ifdef LK_W2_TRACE
+        const uint64_t w0 = __builtin_amdgcn_s_memtime();
+#endif
         while (ldsl_ld(full + s % D) < G::NC * (s / D + 1)) __builtin_amdgcn_s_sleep(1);
+#ifdef LK_W2_TRACE
+        c_wait += __builtin_amdgcn_s_memtime() - w0;
+#endif
       }
-      load(gb + 1, nxt);
+      load(gb + 1, into);
     }
-    compute(gb, cur);
-    cur = nxt;
+    compute(gb, use);
+#if LK_W2_SCHED
+#pragma unroll
+    for (int i = 0; i < MT * NT; i++) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // one tile's MFMA pair
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // then VALU (a lagged tile's scale, decode)
+    }
+#endif
+  };
+  Ops o0, o1;
+  while (ldsl_ld(full) < G::NC) __builtin_amdgcn_s_sleep(1);
+  load(0, o0);
+  for (int gb = 0; gb < nbt; gb += 2) {
+    step(gb, o0, o1);
+    step(gb + 1, o1, o0);
   }
+#ifdef LK_W2_TRACE
+  trace_out();
+#endif
   // outputs: lane holds C'(n = 16·(tn·NT + j) + 4(lane>>4) + e, m = tm·BM + (mw·MT + i)·16 + (lane&15))
   const int npad = g.tiles_n * BN;
 #pragma unroll
