@@ -762,7 +762,7 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
   const int nsuper = ((g.tiles_m + g.sm - 1) / g.sm) * ((g.tiles_n + g.sn - 1) / g.sn);
   g.tasks = nsuper * g.sm * g.sn * slices;
   const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
-  // LK_WIDE2=1: gemm_wide2_kernel (lk_wide2.hpp, dedicated loader waves) on the same tiles; its
+  // LK_WIDE2=1 / 2: gemm_wide2_kernel (lk_wide2.hpp, dedicated loader waves, 4 / 8 consumers) on the same tiles; its
   // Q4 codes are 128 + n, so the activations come in xsplit's q4_order 2 with T = MULT·Σ(hi + lo)
   static const int w2 = [] { const char *e = getenv("LK_WIDE2"); return e ? atoi(e) : 0; }();
   XSplitArgs xw = xa;
@@ -772,7 +772,13 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
   }
   hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xw);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
-  if (w2) hipLaunchKernelGGL((gemm_wide2_kernel<QT>), dim3(grid), dim3(512), Wide2Geom<QT>::LDS, st, g);
+  if (w2 == 2) {
+    using G8 = Wide2Geom<QT, 8>;
+    hipLaunchKernelGGL((gemm_wide2_kernel<QT, 8>), dim3(grid), dim3(G8::NW * 64), G8::LDS, st, g);
+  } else if (w2) {
+    using G4 = Wide2Geom<QT, 4>;
+    hipLaunchKernelGGL((gemm_wide2_kernel<QT, 4>), dim3(grid), dim3(G4::NW * 64), G4::LDS, st, g);
+  }
   else hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
   if (slices > 1) {
     const int64_t threads = (int64_t)g.M * (npad / 4);

@@ -1747,6 +1747,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
 
   const int N16 = 16 * NT;
   const int SH = h == 0 ? NT : 0;  // stores per unit (at least; slices == 1 may store more)
+#ifdef LK_SKP_STALE
+  uint32_t wd0[8][G::WPB] = {};
+#endif
   for (int u = 0; u < nunits; u++) {
     const int slot = u % D;
     f32x4 acc[NT];
@@ -1760,7 +1763,15 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       {
         const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::RPH;
         const uint8_t *bg = bm + (QT == LK_TYPE_Q8_0 ? 8 : 4) * (lane >> 4);
+#ifdef LK_SKP_STALE  // lab skeleton (wrong results): the weight dwords of the first unit only
+        if (u == 0) skinny_read_all<QT, 8, G::WPB, 0>(bm, bg, wd0);
+#pragma unroll
+        for (int b = 0; b < 8; b++)
+#pragma unroll
+          for (int q = 0; q < G::WPB; q++) wd[b][q] = wd0[b][q] + (uint32_t)u;
+#else
         skinny_read_all<QT, 8, G::WPB, 0>(bm, bg, wd);
+#endif
         asm volatile("" ::: "memory");
       }
       if (nbh == 8) skinny_pair_blocks<QT, NT, G::WPB, true, 0>(wd, tl, nbh, lane, xh, xl, acc);

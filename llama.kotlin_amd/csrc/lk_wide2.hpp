@@ -7,14 +7,15 @@
 // every wave issue its share of a stage's DMA and meets the others at two workgroup barriers per
 // stage, so the DMA, the LDS reads and the MFMAs of the workgroup run one after the other (its
 // lab skeleton: DMA + barriers alone 21 µs, + LDS reads 35, + compute 51-55 µs per C5 call).
-// Here the 8 waves split by role, one of each per SIMD:
-//   * waves 0-3, consumers: wave c owns rows [64c, 64c + 64) of the tile and all 64 columns over
-//     the whole K slice (4 x 4 MFMA tiles, no K-group reduction); per stage it waits until the
-//     stage's slot is FULL, reads each block's operands from LDS and computes, and marks the slot
-//     FREE once its last LDS read of the stage has landed;
-//   * waves 4-7, loaders: each issues a fixed quarter of every stage's LDS-DMA instructions,
-//     marks the stage FULL once its own pieces have landed (vmcnt), and refills a slot once the
-//     four consumers have freed it — up to D - 1 stages ahead of the slowest consumer.
+// Here the waves split by role:
+//   * NC = 4 or 8 consumers (one or two per SIMD): consumer c owns rows [64(c % 4), +64) of the
+//     tile and 64·4/NC of its columns over the whole K slice (4 x 4 or 4 x 2 MFMA tiles, no
+//     K-group reduction); per stage it waits until the stage's slot is FULL, reads each block's
+//     operands from LDS and computes, and marks the slot FREE once its last LDS read of the stage
+//     has landed;
+//   * 4 loaders (one per SIMD): each issues a fixed quarter of every stage's LDS-DMA instructions,
+//     marks the stage FULL once its own pieces have landed (vmcnt), and refills a slot once all
+//     consumers have freed it — up to D - 1 stages ahead of the slowest consumer.
 // FULL / FREE are monotonic per-slot LDS counters (4 arrivals per use), so no wave waits at a
 // workgroup barrier after the prologue and the DMA stream overlaps the MFMAs.
 #pragma once
@@ -29,14 +30,30 @@ namespace lk {
 // offset entering through the first MFMA's C input: C = T = −136·S (Q4_0, xsplit mult −136) or
 // C = −128·T with T = S (Q4_1, plus m·T after the MFMA), S = Σ(hi + lo) per (block, column). The
 // stage carries T for both types; Q8_0 keeps gemm_wide_kernel's decode and has no T.
+// LK_W2_MODE (lab skeletons, wrong results): 1 LDS reads only, 2 compute only, 3 reads only and no
+// refills after the first D stages, 4 compute + reads and no refills, 5 the FULL / FREE protocol only
+#ifndef LK_W2_MODE
+#define LK_W2_MODE 0
+#endif
+#ifndef LK_W2_RW  // lab: which operand reads the consumers issue (weights / activations / T)
+#define LK_W2_RW 1
+#endif
+#ifndef LK_W2_RX
+#define LK_W2_RX 1
+#endif
+#ifndef LK_W2_RT
+#define LK_W2_RT 1
+#endif
 #ifndef LK_W2_SCHED
 #define LK_W2_SCHED 1
 #endif
 
-template <int QT> struct Wide2Geom {
+template <int QT, int NC_ = 4> struct Wide2Geom {
   using W = WideGeom<QT>;
-  static constexpr int NC = 4, NL = 4;                          // consumer / loader waves
-  static constexpr int MT = 4, NT = 4, BM = NC * MT * 16, BN = NT * 16;
+  static constexpr int NC = NC_, NL = 4, NW = NC + NL;         // consumer / loader waves
+  // consumer c: rows [64(c % 4), +64), 16-column tiles [NTC(c / 4), +NTC) of the 64-column tile
+  static constexpr int MT = 4, NT = 4, NTC = NT * 4 / NC, BM = 4 * MT * 16, BN = NT * 16;
+  static_assert(NC == 4 || NC == 8, "consumers");
   static constexpr bool HAS_T = QT != LK_TYPE_Q8_0;
   static constexpr int W_BYTES = W::W_BYTES, X_BYTES = W::X_BYTES;
   static constexpr int T_OFF = W_BYTES + X_BYTES;
@@ -59,11 +76,12 @@ template <int QT> struct Wide2Geom {
 __device__ uint64_t *lk_w2trace_buf;
 #endif
 
-template <int QT>
-__global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
-  using G = Wide2Geom<QT>;
+template <int QT, int NC>
+__global__ __launch_bounds__((NC + 4) * 64) void gemm_wide2_kernel(WideArgs g) {
+  using G = Wide2Geom<QT, NC>;
+  static_assert(G::NW == NC + 4, "launch bounds");
   using WG = WideGeom<QT>;
-  constexpr int MT = G::MT, NT = G::NT, BM = G::BM, BN = G::BN, BB = WG::BB, SB = WG::SB, D = G::D;
+  constexpr int MT = G::MT, NT = G::NT, NTC = G::NTC, BM = G::BM, BN = G::BN, BB = WG::BB, SB = WG::SB, D = G::D;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -94,8 +112,8 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
   auto trace_out = [&]() {
     uint64_t *tb = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_w2trace_buf)[0];
     if (lane == 0 && tb) {
-      tb[((size_t)blockIdx.x * 8 + wave) * 2 + 0] = c_wait;
-      tb[((size_t)blockIdx.x * 8 + wave) * 2 + 1] = __builtin_amdgcn_s_memtime() - c_start;
+      tb[((size_t)blockIdx.x * G::NW + wave) * 2 + 0] = c_wait;
+      tb[((size_t)blockIdx.x * G::NW + wave) * 2 + 1] = __builtin_amdgcn_s_memtime() - c_start;
     }
   };
 #endif
@@ -155,7 +173,7 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
       if (lane == 0) __hip_atomic_fetch_add(full + s % D, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       // refill the slot of stage s - 1 once the consumers are done with it
       if (s >= 1 && s - 1 + D < nst) {
-        const int need = G::NC * ((s - 1) / D + 1);
+        const int need = G::NC * ((s - 1) / D + 1);  // every consumer freed it
 #ifdef LK_W2_TRACE
         const uint64_t w0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -163,7 +181,9 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
 #ifdef LK_W2_TRACE
         c_wait += __builtin_amdgcn_s_memtime() - w0;
 #endif
+#if LK_W2_MODE < 3 || LK_W2_MODE == 5
         issue(s - 1 + D);
+#endif
       }
     }
 #ifdef LK_W2_TRACE
@@ -175,24 +195,25 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
   // ---- consumer ----
   // One block of lookahead: block gb + 1's operands are read from LDS while block gb's MFMAs run
   // (a stage's slot is freed once its last block's reads have landed).
-  const int mw = wave;
-  f32x4 acc[MT][NT];
+  const int mw = wave % 4, j0 = (wave / 4) * NTC;
+  f32x4 acc[MT][NTC];
 #pragma unroll
   for (int i = 0; i < MT; i++)
 #pragma unroll
-    for (int j = 0; j < NT; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NTC; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int m = lane & 15, gq = lane >> 4;
   constexpr int WD = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
   struct Ops {
     uint32_t wd[MT][WD];
-    u32x4 xh[NT], xl[NT];
-    f32x4 tq[NT];
+    u32x4 xh[NTC], xl[NTC];
+    f32x4 tq[NTC];
   };
   auto load = [&](int gb, Ops &o) __attribute__((always_inline)) {
     const int s = gb / SB, b = gb % SB, sl = s % D;
     const lu8 *W = sbase + sl * G::STAGE;
     const lu8 *X = W + WG::W_BYTES;
     const int ob = b * BB;
+#if LK_W2_RW
 #pragma unroll
     for (int i = 0; i < MT; i++) {
       const lu8 *rowp = W + ((mw * MT + i) * 16 + m) * WG::WIN;
@@ -212,16 +233,19 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
         o.wd[i][3] = lds32(rowp + ob + 8 * gq + 8);
       }
     }
+#endif
+#if LK_W2_RX
 #pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const LK_LDS u32x4 *xf = (const LK_LDS u32x4 *)(X + ((b * NT + j) * kXSplits) * 1024) + lane;
+    for (int j = 0; j < NTC; j++) {
+      const LK_LDS u32x4 *xf = (const LK_LDS u32x4 *)(X + ((b * NT + j0 + j) * kXSplits) * 1024) + lane;
       o.xh[j] = xf[0];
       o.xl[j] = xf[64];
     }
-    if constexpr (G::HAS_T) {
+#endif
+    if constexpr (G::HAS_T && LK_W2_RT) {
       const LK_LDS float *T = (const LK_LDS float *)(W + G::T_OFF);
 #pragma unroll
-      for (int j = 0; j < NT; j++) o.tq[j] = *(const LK_LDS f32x4 *)(T + b * BN + j * 16 + gq * 4);
+      for (int j = 0; j < NTC; j++) o.tq[j] = *(const LK_LDS f32x4 *)(T + b * BN + (j0 + j) * 16 + gq * 4);
     }
   };
   auto compute = [&](int gb, const Ops &o) __attribute__((always_inline)) {
@@ -244,9 +268,9 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
         s1[i] = h2f(odd ? o.wd[i][0] >> 16 : o.wd[i][0]);
       }
     }
-    f32x4 c0[NT], t[NT];
+    f32x4 c0[NTC], t[NTC];
 #pragma unroll
-    for (int j = 0; j < NT; j++) {
+    for (int j = 0; j < NTC; j++) {
       c0[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       t[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (QT == LK_TYPE_Q4_0) c0[j] = o.tq[j];  // −136·S
@@ -259,7 +283,7 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
     }
     // 16 tiles, each an MFMA pair; a tile's result is scaled into acc LAG tiles later, so the
     // VALU never waits on the MFMA it follows (one in-order wave per SIMD)
-    constexpr int NTL = MT * NT, LAG = 3;
+    constexpr int NTL = MT * NTC, LAG = 3;
     f32x4 pr[LAG + 1];
 #pragma unroll
     for (int k = 0; k < NTL + LAG; k++) {
@@ -288,24 +312,44 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
 #ifdef LK_W2_TRACE
         const uint64_t w0 = __builtin_amdgcn_s_memtime();
 #endif
-        while (ldsl_ld(full + s % D) < G::NC * (s / D + 1)) __builtin_amdgcn_s_sleep(1);
+        while (ldsl_ld(full + s % D) < G::NL * (s / D + 1)) __builtin_amdgcn_s_sleep(1);
 #ifdef LK_W2_TRACE
         c_wait += __builtin_amdgcn_s_memtime() - w0;
 #endif
       }
+#if LK_W2_MODE == 2 || LK_W2_MODE == 5  // lab skeleton: no LDS reads after the first block
+      if (gb < 0) load(gb + 1, into);
+      else into = use;
+#else
       load(gb + 1, into);
+#endif
     }
+#if LK_W2_MODE == 5  // lab skeleton: the FULL / FREE protocol alone
+    acc[0][0].x += __builtin_bit_cast(float, use.wd[0][0] & 0x3FFFFFFFu);
+#elif LK_W2_MODE == 1 || LK_W2_MODE == 3  // lab skeleton: LDS reads only, folded into one accumulator
+    {
+      uint32_t f = 0;
+#pragma unroll
+      for (int i = 0; i < MT; i++)
+#pragma unroll
+        for (int q = 0; q < WD; q++) f ^= use.wd[i][q];
+#pragma unroll
+      for (int j = 0; j < NTC; j++) f ^= use.xh[j][0] ^ use.xl[j][1] ^ __builtin_bit_cast(uint32_t, use.tq[j].x);
+      acc[0][0].x += __builtin_bit_cast(float, f & 0x3FFFFFFFu);
+    }
+#else
     compute(gb, use);
+#endif
 #if LK_W2_SCHED
 #pragma unroll
-    for (int i = 0; i < MT * NT; i++) {
+    for (int i = 0; i < MT * NTC; i++) {
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // one tile's MFMA pair
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // then VALU (a lagged tile's scale, decode)
     }
 #endif
   };
-  Ops o0, o1;
-  while (ldsl_ld(full) < G::NC) __builtin_amdgcn_s_sleep(1);
+  Ops o0{}, o1{};
+  while (ldsl_ld(full) < G::NL) __builtin_amdgcn_s_sleep(1);
   load(0, o0);
   for (int gb = 0; gb < nbt; gb += 2) {
     step(gb, o0, o1);
@@ -321,8 +365,8 @@ __global__ __launch_bounds__(512) void gemm_wide2_kernel(WideArgs g) {
     const int64_t mr = (int64_t)tm * BM + (mw * MT + i) * 16 + (lane & 15);
     if (mr >= g.M) continue;
 #pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const int n0 = tn * BN + j * 16 + 4 * (lane >> 4);
+    for (int j = 0; j < NTC; j++) {
+      const int n0 = tn * BN + (j0 + j) * 16 + 4 * (lane >> 4);
       if (g.slices > 1) {
         *(f32x4 *)(g.partial + (((int64_t)slice * g.M + mr) * npad + n0)) = acc[i][j];
       } else {

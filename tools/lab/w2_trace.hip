@@ -1,5 +1,6 @@
 // w2_trace.hip — lab: gemm_wide2_kernel's waits on C5 (Q4_0 4096 x 4096, N = 512): per wave,
-// cycles spent waiting on FULL (consumers) / FREE (loaders) against its total cycles.
+// cycles spent waiting on FULL (consumers) / FREE (loaders) against its total cycles. LK_WIDE2=2
+// for 8 consumers; -DLK_W2_MODE=1 (LDS reads only) / 2 (compute only) for the skeletons.
 #define LK_W2_TRACE 1
 #include "../../llama.kotlin_amd/csrc/lk_hip.hip"
 
@@ -28,7 +29,8 @@ static lk_tensor mk(int32_t type, int64_t ne0, int64_t ne1, void *data, uint64_t
 }
 
 int main() {
-  setenv("LK_WIDE2", "1", 1);
+  if (!getenv("LK_WIDE2")) setenv("LK_WIDE2", "1", 1);
+  const int NW = atoi(getenv("LK_WIDE2")) == 2 ? 12 : 8, NC = NW - 4;
   const int M = 4096, K = 4096, N = 512;
   const size_t ab = (size_t)M * K / 32 * 18 + 256;
   void *a, *b, *d;
@@ -41,18 +43,18 @@ int main() {
   CK(hipDeviceSynchronize());
   const int grid = 256;
   uint64_t *tb;
-  CK(hipMalloc(&tb, (size_t)grid * 8 * 2 * 8));
-  CK(hipMemset(tb, 0, (size_t)grid * 8 * 2 * 8));
+  CK(hipMalloc(&tb, (size_t)grid * NW * 2 * 8));
+  CK(hipMemset(tb, 0, (size_t)grid * NW * 2 * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(lk_w2trace_buf), &tb, sizeof(tb)));
   lk_mul_mat_device(&A, &B, &Dd, 0);
   CK(hipDeviceSynchronize());
-  std::vector<uint64_t> h((size_t)grid * 16);
+  std::vector<uint64_t> h((size_t)grid * NW * 2);
   CK(hipMemcpy(h.data(), tb, h.size() * 8, hipMemcpyDeviceToHost));
   for (int role = 0; role < 2; role++) {
     std::vector<double> wf, tot;
     for (int g = 0; g < grid; g++)
-      for (int w = role * 4; w < role * 4 + 4; w++) {
-        const uint64_t *q = &h[((size_t)g * 8 + w) * 2];
+      for (int w = role ? NC : 0; w < (role ? NW : NC); w++) {
+        const uint64_t *q = &h[((size_t)g * NW + w) * 2];
         if (q[1]) { wf.push_back((double)q[0] / q[1]); tot.push_back((double)q[1]); }
       }
     std::sort(wf.begin(), wf.end());
