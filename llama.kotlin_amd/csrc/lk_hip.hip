@@ -1591,8 +1591,8 @@ int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor
   const int nbar = (int)stages.size() - 1;
   auto plan = new lk_plan();
   plan->nbar = nbar;
-  if (hipMalloc(&plan->sync, (nbar + 2) * sizeof(unsigned)) != hipSuccess ||
-      hipMemset(plan->sync, 0, (nbar + 2) * sizeof(unsigned)) != hipSuccess) {
+  const size_t sync_bytes = (size_t)(nbar * 9 + 2) * kChainLine * sizeof(unsigned);
+  if (hipMalloc(&plan->sync, sync_bytes) != hipSuccess || hipMemset(plan->sync, 0, sync_bytes) != hipSuccess) {
     lk_plan_destroy(plan);
     return fail(LK_ERR_DEVICE, "chain: sync alloc");
   }
@@ -1638,9 +1638,10 @@ int lk_plan_chain_timed_out(lk_plan *plan) {
   if (!plan || !plan->sync) return 0;
   unsigned flag = 0;
   if (hipDeviceSynchronize() != hipSuccess) return fail(LK_ERR_DEVICE, "chain: sync");
-  if (hipMemcpy(&flag, plan->sync + plan->nbar + 1, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess) return fail(LK_ERR_DEVICE, "chain: flag");
+  const int words = (plan->nbar * 9 + 2) * kChainLine;
+  if (hipMemcpy(&flag, plan->sync + words - kChainLine, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess) return fail(LK_ERR_DEVICE, "chain: flag");
   if (flag) {
-    (void)hipMemset(plan->sync, 0, (plan->nbar + 2) * sizeof(unsigned));
+    (void)hipMemset(plan->sync, 0, (size_t)words * sizeof(unsigned));
     return 1;
   }
   return 0;

@@ -300,11 +300,13 @@ struct StreamWork {
   int64_t dst_row_stride;
   int32_t K, row_begin, row_end, count;
   // chain plans (lk_plan_create_chain): barrier > 0 puts grid barrier #barrier−1 before this
-  // segment; sync = [nbar] arrival counters, [nbar] exit counter, [nbar + 1] timeout flag
+  // segment; sync = per barrier 9 words (top, 8 shards), then the exit counter and the timeout
+  // flag, each word on a 128-B line of its own (kChainLine words apart)
   int32_t barrier, nbar;
   unsigned *sync;
 };
 static_assert(sizeof(StreamWork) == 64, "one s_load_dwordx16");
+constexpr int kChainLine = 32;  // chain sync words: one per 128-B line
 
 template <int QT, int CPL> struct StreamGeom {
   static constexpr int PB = 2 * QTraits<QT>::BB;         // bytes per block pair
@@ -528,6 +530,34 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(xv + p * 16 + t), (LK_LDS void *)(lds + k * 64), 16, 0, 0);
       }
     };
+    // chain plans: the node's activations by sc1 loads to registers (they may be another
+    // workgroup's outputs of this launch, stored write-through), four per wave and round, then
+    // into the image as dma_x places them (image float4 64k + lane from instruction k, by wave k % 8)
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void *)x_node, 0, K * 4, 0x00020000);
+    const int xinst = (NP + 3) / 4, xrounds = (xinst + 4 * kStreamWaves - 1) / (4 * kStreamWaves);
+    auto x_issue = [&](int r, f32x4 (&xv)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int k = min(wave + kStreamWaves * (4 * r + q), xinst - 1), i = k * 64 + lane;
+        const int p = min(i >> 4, NP - 1), t = (i & 15) ^ ((i >> 4) & 15);
+        xv[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (p * 16 + t) * 16, 0, 16));
+      }
+    };
+    auto x_store = [&](int r, const f32x4 (&xv)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int k = wave + kStreamWaves * (4 * r + q);
+        if (k < xinst) lds[k * 64 + lane] = xv[q];
+      }
+    };
+    auto load_x_sc1 = [&]() __attribute__((always_inline)) {  // every round after all older loads
+      for (int r = 0; r < xrounds; r++) {
+        f32x4 xv[4];
+        x_issue(r, xv);
+        wait_vmcnt<0>();
+        x_store(r, xv);
+      }
+    };
     auto weight_prologue = [&](bool with_x) __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < G::D; k++) {
@@ -544,36 +574,60 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       islot = 0;  // the next unit to issue is unit D, slot D % D
     };
     if (bar) {
-      // chain plans: grid barrier #bar−1 between dependent stages, inside the launch.
-      // 1. this workgroup's stores of the previous stage have completed; one lane releases
-      //    them (L2 write-back) and arrives
-      wait_vmcnt<0>();
+      // chain plans: grid barrier #bar−1 between dependent stages, inside the launch. The previous
+      // stage's outputs were stored write-through (sc1) and this stage reads them with sc1 loads
+      // only, so neither side needs an L2 write-back or invalidate (MI355X_MICROARCH.md, visibility:
+      // valid forms, row 1).
+      // 1. every wave's stores have completed; one lane arrives on this workgroup's shard (8 shards,
+      //    one 128-B line each); the shard's last arriver arrives on the top word
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      unsigned *bsync = sync + (bar - 1) * kChainLine * 9;
       if (wave == 0 && lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(sync + bar - 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int sh = (int)blockIdx.x % 8;
+        const unsigned shn = (gridDim.x - sh + 7) / 8;  // workgroups of shard sh
+        const unsigned prev = __hip_atomic_fetch_add(bsync + (1 + sh) * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == shn - 1) __hip_atomic_fetch_add(bsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       // 2. the weights do not depend on the previous stage: their stream starts now
       weight_prologue(false);
-      // 3. one lane waits for every workgroup (bounded: a grid that is not co-resident sets the
-      //    timeout flag and runs on instead of hanging), then acquires for the whole CU
+      // 3. one lane waits until all 8 shards are complete (bounded: a grid that is not
+      //    co-resident sets the timeout flag and runs on instead of hanging)
+#ifndef LK_CHAIN_NOWAIT  // lab skeleton (wrong results): the stages run on without waiting
       if (wave == 0 && lane == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(sync + bar - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+        const unsigned nsh = gridDim.x < 8 ? gridDim.x : 8;
+        while (__hip_atomic_load(bsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nsh) {
           __builtin_amdgcn_s_sleep(2);
           if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 200 ms at 100 MHz
-            __hip_atomic_store(sync + nbar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sync + (nbar * 9 + 1) * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+#endif
+      asm volatile("" ::: "memory");  // the loads below stay after the poll
       __builtin_amdgcn_s_barrier();
-      // 4. the stage's activations (the youngest DMA: wait for everything)
-      dma_x();
-      wait_vmcnt<0>();
+      // 4. the stage's activations (sc1 loads: the youngest, so wait for all)
+      load_x_sc1();
+      wait_lgkmcnt0();
+      __builtin_amdgcn_s_barrier();
+    } else if (sync) {  // chain plans, a later segment of a stage (or stage 0): no grid barrier
+      if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
+      {  // the first round of activation loads ahead of the weight prologue, waited for alone
+        f32x4 xv[4];
+        x_issue(0, xv);
+        weight_prologue(false);
+        wait_vmcnt<G::D * G::L>();
+        x_store(0, xv);
+      }
+      for (int r = 1; r < xrounds; r++) {
+        f32x4 xv[4];
+        x_issue(r, xv);
+        wait_vmcnt<0>();
+        x_store(r, xv);
+      }
+      wait_lgkmcnt0();
       __builtin_amdgcn_s_barrier();
     } else {
     if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
@@ -664,19 +718,23 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 #else
       const float tot = dpp_sum(acc);
 #endif
-      if (lane == 63) out[(int64_t)row * dst_stride] = tot;
+      if (lane == 63) {
+        if (sync) __hip_atomic_store(out + (int64_t)row * dst_stride, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
+        else out[(int64_t)row * dst_stride] = tot;
+      }
     }
   }
   if (sync) {
     // chain plans: the workgroup that leaves last (every workgroup has passed every barrier)
     // re-arms the counters for the next launch (stream order makes the stores visible to it)
-    wait_vmcnt<0>();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (wave == 0 && lane == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(sync + nbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == gridDim.x - 1) {
-        for (int b = 0; b <= nbar; b++) __hip_atomic_store(sync + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    if (wave == 0) {
+      unsigned prev = 0;
+      if (lane == 0) prev = __hip_atomic_fetch_add(sync + nbar * 9 * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      prev = __shfl(prev, 0, kWave);
+      if (prev == gridDim.x - 1)
+        for (int b = lane; b <= nbar * 9; b += kWave) __hip_atomic_store(sync + b * kChainLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   LK_TRACE(3);
