@@ -1689,6 +1689,9 @@ __device__ __forceinline__ void lds_st(int *p, int v) {
   asm volatile("" ::: "memory");
 }
 
+#ifndef LK_SKP_EARLY
+#define LK_SKP_EARLY 0
+#endif
 template <int QT, int NT>
 __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   using G = SkinnyPairGeom<QT, NT>;
@@ -1739,6 +1742,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     }
   };
 
+  // 0. (lab, LK_SKP_EARLY=1) the weight ring first, so its HBM round trip overlaps the
+  //    activation loads (their compiler waits then also wait for these older DMAs): measured
+  //    slower on C3, 24.0 vs 23.1 us per call (the activation loads queue behind the burst)
+  if (LK_SKP_EARLY && myL)
+    for (int u = 0; u < min(D, nunits); u++) issue(u, u);
   // 1. activations of the slice -> LDS fragments, as gemm_skinny_kernel (compiler-visible loads:
   //    issued before the weight ring, so waiting for them never waits for it)
   float v[G::FPW][8];
@@ -1785,8 +1793,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       if (lane < 16) tlds[f * 16 + lane] = part;
     }
   }
-  // 2. the weight ring
-  if (myL)
+  // 2. the weight ring, after the split (LK_SKP_EARLY=0, the default)
+  if (!LK_SKP_EARLY && myL)
     for (int u = 0; u < min(D, nunits); u++) issue(u, u);
   wait_lgkmcnt0();
   __builtin_amdgcn_s_barrier();  // fragments and flags visible (bare: the ring stays in flight)
