@@ -1626,13 +1626,28 @@ template <int J> __device__ __forceinline__ void wait_vmcnt_rt(int x) {
 }
 
 // Block B (0..7) of this wave's half: x held as [8][NT]; T (Q4_1) indexed by the slice block.
+// Lab skeletons (LK_SKP_SKEL, wrong results; tools/lab/skp_skel.sh): 1 no MFMAs, 2 no decode,
+// 3 no ring refills, 4 no accumulator hand-off, 5 no decode / MFMA / scale.
+#ifndef LK_SKP_SKEL
+#define LK_SKP_SKEL 0
+#endif
 template <int QT, int NT, int B, int WPB>
 __device__ __forceinline__ void skinny_pair_block(const uint32_t (&w)[WPB], const float *tl, int lane, const u32x4 (&xh)[8][NT],
                                                   const u32x4 (&xl)[8][NT], f32x4 (&acc)[NT]) {
   constexpr int OB = B * QTraits<QT>::BB;
   bf16x8 wf;
   float s1, s2 = 0.f;
+#if LK_SKP_SKEL == 5
+  acc[0].x += __builtin_bit_cast(float, w[0] & 0x3FFFFFFFu);
+  return;
+#endif
+#if LK_SKP_SKEL == 2
+  wf = __builtin_bit_cast(bf16x8, u32x4{w[WPB - 1], w[WPB - 1] ^ 1u, w[WPB - 1] ^ 2u, w[WPB - 1] ^ 3u});
+  s1 = __builtin_bit_cast(float, w[0] & 0x3FFFFFFFu);
+  if constexpr (false) {
+#else
   if constexpr (QT == LK_TYPE_Q4_1) {
+#endif
     wf = Q4Frag<0>::make(w[1]);
     s1 = 512.f * h2f(w[0]);
     s2 = h2f(w[0] >> 16);
@@ -1655,9 +1670,13 @@ __device__ __forceinline__ void skinny_pair_block(const uint32_t (&w)[WPB], cons
   }
 #pragma unroll
   for (int j = 0; j < NT; j++) {
+#if LK_SKP_SKEL == 1
+    f32x4 p = __builtin_bit_cast(f32x4, wf);
+#else
     f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf, f32x4{0.f, 0.f, 0.f, 0.f},
                                                       0, 0, 0);
     p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
+#endif
     f32x4 t = {0.f, 0.f, 0.f, 0.f};
     if constexpr (QT == LK_TYPE_Q4_1) t = *(const f32x4 *)(tl + (B * NT + j) * 16 + (lane >> 4) * 4);
     accumulate_s<QT == LK_TYPE_Q4_1>(acc[j], s1, s2, p, t);
@@ -1692,6 +1711,12 @@ __device__ __forceinline__ void lds_st(int *p, int v) {
 #ifndef LK_SKP_EARLY
 #define LK_SKP_EARLY 0
 #endif
+#ifndef LK_SKP_PRIO
+#define LK_SKP_PRIO 0
+#endif
+#ifndef LK_SKP_STAGGER
+#define LK_SKP_STAGGER 0
+#endif
 template <int QT, int NT>
 __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   using G = SkinnyPairGeom<QT, NT>;
@@ -1705,6 +1730,17 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int p = wave & 3, h = wave >> 2;
   uint8_t *ring = smem + G::XB + G::TB + G::EB + G::FB + wave * D * G::SLOT;
+#ifdef LK_SKINNY_TRACE  // tools/lab/skinny_trace.hip (PAIR=1): the same stamps as gemm_skinny_kernel
+  uint64_t *const strace = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_strace_buf)[0];
+#define LK_PTRACE(slot_)                                                                                     \
+  do {                                                                                                      \
+    if (lane == 0 && strace)                                                                                \
+      strace[((size_t)blockIdx.x * NW + wave) * 8 + (slot_)] = __builtin_amdgcn_s_memrealtime();             \
+  } while (0)
+#else
+#define LK_PTRACE(slot_) do {} while (0)
+#endif
+  LK_PTRACE(0);
   // XCD-aware task order, as gemm_skinny_kernel
   const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
   if (task >= g.tasks) return;  // grid padding (before any barrier: the whole workgroup leaves)
@@ -1793,6 +1829,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       if (lane < 16) tlds[f * 16 + lane] = part;
     }
   }
+  LK_PTRACE(1);
   // 2. the weight ring, after the split (LK_SKP_EARLY=0, the default)
   if (!LK_SKP_EARLY && myL)
     for (int u = 0; u < min(D, nunits); u++) issue(u, u);
@@ -1810,6 +1847,18 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       xl[b][j] = xf[64];
     }
   const float *tl = tlds + 8 * h * NT * 16;
+  LK_PTRACE(2);
+  // lab: LK_SKP_PRIO 1 raises the h = 1 wave's issue priority, 2 the h = 0 wave's; LK_SKP_STAGGER
+  // delays the h = 0 wave's first unit (s_sleep units of 64 cycles) so the pair's MFMA phases
+  // interleave instead of contending for the SIMD's one MFMA pipe
+#if LK_SKP_PRIO == 1
+  if (h == 1) __builtin_amdgcn_s_setprio(1);
+#elif LK_SKP_PRIO == 2
+  if (h == 0) __builtin_amdgcn_s_setprio(1);
+#endif
+#if LK_SKP_STAGGER
+  if (h == 0) for (int i = 0; i < LK_SKP_STAGGER; i++) __builtin_amdgcn_s_sleep(1);
+#endif
 
   const int N16 = 16 * NT;
   const int SH = h == 0 ? NT : 0;  // stores per unit (at least; slices == 1 may store more)
@@ -1825,6 +1874,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       // ops younger than this unit's DMA: its successors already issued, and the stores since
       wait_vmcnt_rt<G::MAXW>(myL * min(D - 1, nunits - 1 - u) + min(u, D) * SH);
       asm volatile("" ::: "memory");
+      if (u == 0) LK_PTRACE(3);
       uint32_t wd[8][G::WPB];
       {
         const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::RPH;
@@ -1843,19 +1893,23 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       if (nbh == 8) skinny_pair_blocks<QT, NT, G::WPB, true, 0>(wd, tl, nbh, lane, xh, xl, acc);
       else skinny_pair_blocks<QT, NT, G::WPB, false, 0>(wd, tl, nbh, lane, xh, xl, acc);
       wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
-      if (u + D < nunits) issue(u + D, slot);
+      if (u + D < nunits && LK_SKP_SKEL != 3) issue(u + D, slot);
+      if (u == 0) LK_PTRACE(7);
     }
     f32x4 *xb = xch + ((u & 1) * 4 + p) * NT * 64 + lane;
     if (h == 1) {
+      if (LK_SKP_SKEL == 4) continue;
       // the partner has consumed unit u − 2 (this parity's previous contents)
       while (lds_ld(flags + 8 + p) < u - 1) __builtin_amdgcn_s_sleep(1);
 #pragma unroll
       for (int j = 0; j < NT; j++) xb[j * 64] = acc[j];
       lds_st(flags + 2 * p + (u & 1), u + 1);
     } else {
-      while (lds_ld(flags + 2 * p + (u & 1)) != u + 1) __builtin_amdgcn_s_sleep(1);
+      if (LK_SKP_SKEL != 4) {
+        while (lds_ld(flags + 2 * p + (u & 1)) != u + 1) __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-      for (int j = 0; j < NT; j++) acc[j] += xb[j * 64];
+        for (int j = 0; j < NT; j++) acc[j] += xb[j * 64];
+      }
       lds_st(flags + 8 + p, u + 1);
       // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
       const int t = t0 + p + u * 4;
@@ -1873,8 +1927,12 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
         }
       }
     }
+    if (u == 0) LK_PTRACE(4);
   }
+  LK_PTRACE(5);
   wait_vmcnt<0>();
+  LK_PTRACE(6);
+#undef LK_PTRACE
 }
 
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------

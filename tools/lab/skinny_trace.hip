@@ -1,6 +1,7 @@
 // skinny_trace.hip — lab: per-wave timeline of gemm_skinny_kernel (s_memrealtime, 100 MHz):
 // 0 entry, 1 activation loads converted, 2 after the barrier, 3 first unit landed,
 // 4 first unit done, 5 loop done, 6 drained. usage: skinny_trace M K N [waves]
+// PAIR=1: gemm_skinny_pair_kernel (Q4_0, N > 16) instead; LK_SKP_SKEL builds its skeletons.
 #define LK_SKINNY_TRACE 1
 #ifndef LK_SKINNY_NT
 #define LK_SKINNY_NT 0
@@ -8,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -25,9 +27,9 @@ __global__ void fill(uint32_t *p, size_t n, uint32_t seed) {
     p[i] = ((uint32_t)i * 2654435761u ^ seed) & 0x3BFF3BFFu;  // finite halves
 }
 
-template <int NT>
+template <int NT, bool PAIR>
 void run(int M, int K, int N) {
-  using SG = lk::SkinnyGeom<LK_TYPE_Q4_0, NT>;
+  using SG = std::conditional_t<PAIR, lk::SkinnyPairGeom<LK_TYPE_Q4_0, NT>, lk::SkinnyGeom<LK_TYPE_Q4_0, NT>>;
   constexpr int NW = SG::NW;
   const int nblk = K / 32, slices = (nblk + SG::SB - 1) / SG::SB, ntile = (M + 15) / 16;
   int ranges = std::max(1, std::min(ntile, (256 + slices - 1) / slices));
@@ -65,7 +67,8 @@ void run(int M, int K, int N) {
     const int reps = pass ? 1 : 3 * rot;
     for (int i = 0; i < reps; i++) {
       g.a = as[i % rot];
-      hipLaunchKernelGGL((lk::gemm_skinny_kernel<LK_TYPE_Q4_0, NT>), dim3(grid), dim3(NW * 64), SG::LDS, 0, g);
+      if constexpr (PAIR) hipLaunchKernelGGL((lk::gemm_skinny_pair_kernel<LK_TYPE_Q4_0, NT>), dim3(grid), dim3(NW * 64), SG::LDS, 0, g);
+      else hipLaunchKernelGGL((lk::gemm_skinny_kernel<LK_TYPE_Q4_0, NT>), dim3(grid), dim3(NW * 64), SG::LDS, 0, g);
     }
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
@@ -93,7 +96,9 @@ void run(int M, int K, int N) {
 
 int main(int argc, char **argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 11008, K = argc > 2 ? atoi(argv[2]) : 4096, N = argc > 3 ? atoi(argv[3]) : 32;
-  if (N > 16) run<2>(M, K, N);
-  else run<1>(M, K, N);
+  const bool pair = getenv("PAIR") && atoi(getenv("PAIR"));
+  if (pair) run<2, true>(M, K, N);
+  else if (N > 16) run<2, false>(M, K, N);
+  else run<1, false>(M, K, N);
   return 0;
 }
