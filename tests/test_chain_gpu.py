@@ -42,6 +42,9 @@ CHAINS = [
     (2, [1024, 512, 2048, 1024, 256, 4096], [1, 2, 1, 1, 3]),
     (6, [2048, 2048, 1024], [2, 1]),                # Q8_0
     (3, [4096, 384, 4096], [1, 1]),                 # Q4_1, a 384-row stage: most waves hold no row
+    # uneven arrivals: a 256-row stage between two long ones (16 workgroups hold rows there, the
+    # rest arrive at once), then an 11008-wide activation read right after it
+    (2, [4096, 11008, 256, 11008, 4096], [1, 1, 1, 1]),
 ]
 
 
