@@ -369,7 +369,10 @@ struct GemmScratch {
   void *frag = nullptr; size_t frag_bytes = 0;
   void *partial = nullptr; size_t partial_bytes = 0;
   int32_t *counter = nullptr; size_t counter_n = 0;
+  unsigned *rsync = nullptr;  // fused split-K arrival counters: kRsyncRows rows of rsync_line lines
+  int rsync_line = 0;
 };
+constexpr int kRsyncRows = 64;  // slices values 1..64 (K <= 32768 on the skinny path)
 GemmScratch &gemm_scratch() {
   static GemmScratch per_dev[64];
   int dev = 0;
@@ -547,19 +550,38 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   const int nblk = g.K / 32;
   const int slices = (nblk + SG::SB - 1) / SG::SB;
   const int ntile = (g.M + 15) / 16;
-  int ranges = std::max(1, std::min(ntile, (cu_count() + slices - 1) / slices));
+  // fused split-K reduction (the default; LK_SKP_UNFUSED=1: splitk_reduce_kernel after): every
+  // task co-resident (at most one per CU: the kernel's LDS admits one), slabs addressable by a
+  // 32-bit buffer offset
+  static const bool unfused = getenv("LK_SKP_UNFUSED") != nullptr;
+  const int cu = cu_count();
+  const size_t slab_bytes = (size_t)slices * g.M * 16 * NT * sizeof(float);
+  const bool fuse = !unfused && slices > 1 && slices <= kRsyncRows && slices <= cu && slab_bytes < (1ull << 31);
+  int ranges = std::max(1, std::min(ntile, fuse ? cu / slices : (cu + slices - 1) / slices));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   g.slices = slices;
   if (slices > 1) {
-    const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
+    const int rc = grow(&S.partial, &S.partial_bytes, slab_bytes);
     if (rc) return rc;
     g.partial = (float *)S.partial;
   }
   g.tasks = ranges * slices;
+  g.rsync = nullptr;
+  if (fuse) {
+    if (!S.rsync) {
+      const int line = (cu + 7) / 8 * 8 + 1;  // a counter per range + the timeout flag after the grid
+      const size_t bytes = (size_t)kRsyncRows * line * kChainLine * sizeof(unsigned);
+      HIP_TRY(hipMalloc((void **)&S.rsync, bytes));
+      HIP_TRY(hipMemset(S.rsync, 0, bytes));
+      S.rsync_line = line;
+    }
+    g.rsync = S.rsync + (size_t)(slices - 1) * S.rsync_line * kChainLine;
+  }
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_skinny_pair_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
-  if (slices > 1) {
+  static const bool skip_reduce = getenv("LK_LAB_SKIP_REDUCE") != nullptr;  // lab (wrong results): the reduce's share
+  if (slices > 1 && !fuse && !skip_reduce) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
                        slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);

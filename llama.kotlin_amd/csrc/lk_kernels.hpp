@@ -1291,6 +1291,11 @@ struct SkinnyArgs {
   float *partial;          // [slices][M][16·NT] when slices > 1
   int32_t M, N, K;
   int32_t slices, tiles_per_range, tasks;  // tasks = ranges·slices (the grid is padded to 8)
+  // gemm_skinny_pair_kernel's fused split-K reduction (null: splitk_reduce_kernel runs after):
+  // one arrival counter per range on its own 128-B line (kChainLine words apart), a counter row
+  // per `slices` value so every counter stays a multiple of slices between calls; the word after
+  // the row's last counter is the timeout flag
+  unsigned *rsync;
 };
 
 // s_waitcnt vmcnt(BASE + j·STEP) for a run-time j in [0, J].
@@ -1863,6 +1868,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
 #endif
 
   const int N16 = 16 * NT;
+  // the partial slabs as a buffer (fused reduction: sc1 stores and loads; the host checks the size)
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
   const int SH = h == 0 ? NT : 0;  // stores per unit (at least; slices == 1 may store more)
 #ifdef LK_SKP_STALE
   uint32_t wd0[8][G::WPB] = {};
@@ -1920,7 +1928,12 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       for (int j = 0; j < NT; j++) {
         const int n0 = 16 * j + 4 * (lane >> 4);
         if (g.slices > 1) {
-          if (m < g.M) *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = acc[j];
+          if (m < g.M) {
+            if (g.rsync)  // write-through (sc1): another workgroup of the range adds it up
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j]), prs,
+                                                     (int)((((int64_t)slice * g.M + m) * N16 + n0) * 4), 0, 16);
+            else *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = acc[j];
+          }
         } else if (m < g.M) {
           const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
 #pragma unroll
@@ -1935,6 +1948,58 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   wait_vmcnt<0>();
   LK_PTRACE(6);
 #undef LK_PTRACE
+  if (g.rsync) {
+    // fused split-K reduction: every wave's slab stores have completed (write-through); one lane
+    // arrives on the range's counter and waits for the range's other slices (all tasks are
+    // co-resident: the host launches at most one per CU), then the workgroup adds its share of
+    // the range's rows, slabs in slice order (as splitk_reduce_kernel: bit-identical)
+    __builtin_amdgcn_s_barrier();
+    if (wave == 0 && lane == 0) {
+      unsigned *c = g.rsync + range * kChainLine;
+      const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (old / (unsigned)g.slices + 1u) * (unsigned)g.slices;
+      const uint64_t ts = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - ts > 20000000ull) {  // 200 ms: flag, run on, never hang
+          __hip_atomic_store(g.rsync + (int64_t)gridDim.x * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    asm volatile("" ::: "memory");  // the slab loads stay after the poll
+    __builtin_amdgcn_s_barrier();
+    const int m0 = t0 * 16, m1 = min(t1 * 16, g.M);
+    const int per = (m1 - m0 + g.slices - 1) / g.slices;
+    const int r0 = min(m0 + slice * per, m1), r1 = min(r0 + per, m1);
+    const int c4 = N16 / 4;
+    for (int idx = (int)threadIdx.x; idx < (r1 - r0) * c4; idx += NW * 64) {
+      const int64_t m = r0 + idx / c4;
+      const int n0 = (idx % c4) * 4;
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < g.slices; b += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if (b + i < g.slices)
+            v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)(b + i) * g.M + m) * N16 + n0) * 4), 0, 16));
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if (b + i < g.slices) {
+            if (b + i == 0) sum = v[i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
+            else { sum.x += v[i].x; sum.y += v[i].y; sum.z += v[i].z; sum.w += v[i].w; }
+          }
+      }
+      const float e4[4] = {sum.x, sum.y, sum.z, sum.w};
+      if (g.d_nb0 == 4 && n0 + 4 <= g.N && (((uintptr_t)(g.dst + m * g.d_nb1 + n0 * 4)) & 15) == 0) {
+        *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = sum;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+      }
+    }
+  }
 }
 
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------
