@@ -373,12 +373,34 @@ struct GemmScratch {
   int rsync_line = 0;
 };
 constexpr int kRsyncRows = 64;  // slices values 1..64 (K <= 32768 on the skinny path)
+
 GemmScratch &gemm_scratch() {
   static GemmScratch per_dev[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   return per_dev[dev];
 }
+// Fused split-K reduction (lk_kernels.hpp splitk_fused_reduce) for `slices` slices of slab_bytes:
+// the counter row to pass, or null (splitk_reduce_kernel runs after: LK_SKP_UNFUSED=1, one slice,
+// too many slices, or slabs beyond a 32-bit buffer offset). The caller keeps ranges·slices <=
+// cu_count() so every task is co-resident (one workgroup per CU).
+int fused_rsync(int slices, size_t slab_bytes, unsigned **out) {
+  static const bool unfused = getenv("LK_SKP_UNFUSED") != nullptr;
+  *out = nullptr;
+  const int cu = cu_count();
+  if (unfused || slices <= 1 || slices > kRsyncRows || slices > cu || slab_bytes >= (1ull << 31)) return LK_OK;
+  GemmScratch &S = gemm_scratch();
+  if (!S.rsync) {
+    const int line = (cu + 7) / 8 * 8 + 1;  // a counter per range + the timeout flag after the grid
+    const size_t bytes = (size_t)kRsyncRows * line * kChainLine * sizeof(unsigned);
+    HIP_TRY(hipMalloc((void **)&S.rsync, bytes));
+    HIP_TRY(hipMemset(S.rsync, 0, bytes));
+    S.rsync_line = line;
+  }
+  *out = S.rsync + (size_t)(slices - 1) * S.rsync_line * kChainLine;
+  return LK_OK;
+}
+
 int grow(void **p, size_t *have, size_t want) {
   if (*have >= want) return LK_OK;
   if (*p) HIP_TRY(hipFree(*p));
@@ -550,13 +572,12 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   const int nblk = g.K / 32;
   const int slices = (nblk + SG::SB - 1) / SG::SB;
   const int ntile = (g.M + 15) / 16;
-  // fused split-K reduction (the default; LK_SKP_UNFUSED=1: splitk_reduce_kernel after): every
-  // task co-resident (at most one per CU: the kernel's LDS admits one), slabs addressable by a
-  // 32-bit buffer offset
-  static const bool unfused = getenv("LK_SKP_UNFUSED") != nullptr;
+  // fused split-K reduction unless LK_SKP_UNFUSED=1 (fused_rsync): every task co-resident
   const int cu = cu_count();
   const size_t slab_bytes = (size_t)slices * g.M * 16 * NT * sizeof(float);
-  const bool fuse = !unfused && slices > 1 && slices <= kRsyncRows && slices <= cu && slab_bytes < (1ull << 31);
+  unsigned *rsync = nullptr;
+  if (int rc = fused_rsync(slices, slab_bytes, &rsync)) return rc;
+  const bool fuse = rsync != nullptr;
   int ranges = std::max(1, std::min(ntile, fuse ? cu / slices : (cu + slices - 1) / slices));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
@@ -567,17 +588,7 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
     g.partial = (float *)S.partial;
   }
   g.tasks = ranges * slices;
-  g.rsync = nullptr;
-  if (fuse) {
-    if (!S.rsync) {
-      const int line = (cu + 7) / 8 * 8 + 1;  // a counter per range + the timeout flag after the grid
-      const size_t bytes = (size_t)kRsyncRows * line * kChainLine * sizeof(unsigned);
-      HIP_TRY(hipMalloc((void **)&S.rsync, bytes));
-      HIP_TRY(hipMemset(S.rsync, 0, bytes));
-      S.rsync_line = line;
-    }
-    g.rsync = S.rsync + (size_t)(slices - 1) * S.rsync_line * kChainLine;
-  }
+  g.rsync = rsync;
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_skinny_pair_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
   static const bool skip_reduce = getenv("LK_LAB_SKIP_REDUCE") != nullptr;  // lab (wrong results): the reduce's share
@@ -667,7 +678,12 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
   const int slices = (int)((nblk + SG::SB - 1) / SG::SB);
   const int ntile = (g.M + 15) / 16;
-  int ranges = std::max(1, std::min(ntile, (cu_count() + slices - 1) / slices));
+  // fused split-K reduction (gemm_sk_kernel; the one-wave lab kernel keeps the reduce launch)
+  const int cu = cu_count();
+  unsigned *rsync = nullptr;
+  if (!SOLO)
+    if (int rf = fused_rsync(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), &rsync)) return rf;
+  int ranges = std::max(1, std::min(ntile, rsync ? cu / slices : (cu + slices - 1) / slices));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   g.slices = slices;
@@ -677,6 +693,7 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
     g.partial = (float *)S.partial;
   }
   g.tasks = ranges * slices;
+  g.rsync = rsync;
   // dense, 16-B aligned B (every Llama activation): the GEMM splits its slice itself (no xsplit
   // launch); LK_SK_XSPLIT=1 forces the separate split (lab A/B)
   static const bool force_xsplit = getenv("LK_SK_XSPLIT") != nullptr;
@@ -690,7 +707,7 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   } else {
     hipLaunchKernelGGL((gemm_sk_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
   }
-  if (slices > 1) {
+  if (slices > 1 && !rsync) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
                        slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);

@@ -1590,6 +1590,72 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
 #undef LK_STRACE
 }
 
+// Fused split-K reduction (gemm_skinny_pair_kernel, gemm_sk_kernel): called by every wave of a
+// task once its partial slab rows [m0, m1) of slice `slice` are stored write-through (sc1) and
+// drained. One lane arrives on the row range's counter and waits for the range's other slices (the
+// host launches every task co-resident: at most one workgroup per CU), then the workgroup adds its
+// 1/slices share of the range's rows, slabs in slice order — the order of splitk_reduce_kernel, so
+// the result is bit-identical to it. rsync: the counter row of this `slices` value (each call adds
+// exactly `slices` per range, so every counter is a multiple of slices between calls); the word
+// gridDim.x lines on is a timeout flag (a 200 ms bound instead of a hang).
+template <int NW>
+__device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amdgpu_buffer_rsrc_t prs, int range, int slice,
+                                                    int slices, int m0, int m1, int M, int N, int N16, uint8_t *dst,
+                                                    int64_t d_nb0, int64_t d_nb1, int wave, int lane) {
+  __builtin_amdgcn_s_barrier();
+  if (wave == 0 && lane == 0) {
+    unsigned *c = rsync + range * kChainLine;
+    const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (old / (unsigned)slices + 1u) * (unsigned)slices;
+    const uint64_t ts = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - ts > 20000000ull) {  // 200 ms at 100 MHz
+        __hip_atomic_store(rsync + (int64_t)gridDim.x * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  asm volatile("" ::: "memory");  // the slab loads stay after the poll
+  __builtin_amdgcn_s_barrier();
+  const int per = (m1 - m0 + slices - 1) / slices;
+  const int r0 = min(m0 + slice * per, m1), r1 = min(r0 + per, m1);
+  const int c4 = N16 / 4;
+  for (int idx = (int)threadIdx.x; idx < (r1 - r0) * c4; idx += NW * 64) {
+    const int64_t m = r0 + idx / c4;
+    const int n0 = (idx % c4) * 4;
+    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < slices; b += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if (b + i < slices)
+          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)(b + i) * M + m) * N16 + n0) * 4), 0, 16));
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if (b + i < slices) {
+          if (b + i == 0) sum = v[i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
+          else { sum.x += v[i].x; sum.y += v[i].y; sum.z += v[i].z; sum.w += v[i].w; }
+        }
+    }
+    const float e4[4] = {sum.x, sum.y, sum.z, sum.w};
+    if (d_nb0 == 4 && n0 + 4 <= N && (((uintptr_t)(dst + m * d_nb1 + n0 * 4)) & 15) == 0) {
+      *(f32x4 *)(dst + m * d_nb1 + n0 * 4) = sum;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (n0 + q < N) *(float *)(dst + m * d_nb1 + (n0 + q) * d_nb0) = e4[q];
+    }
+  }
+}
+
+// a partial slab's f32x4: write-through when the reduction is fused (another workgroup reads it)
+__device__ __forceinline__ void store_partial(bool fused, const __amdgpu_buffer_rsrc_t prs, float *partial, int64_t idx,
+                                              f32x4 v) {
+  if (fused) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), prs, (int)(idx * 4), 0, 16);
+  else *(f32x4 *)(partial + idx) = v;
+}
+
 // ---- skinny GEMM on wave pairs (Q4_0 / Q4_1, 17 <= N <= 32) -------------------------------
 //
 // gemm_skinny_kernel runs one wave per SIMD (all of the slice's x-fragments, 256 VGPRs at
@@ -1928,12 +1994,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       for (int j = 0; j < NT; j++) {
         const int n0 = 16 * j + 4 * (lane >> 4);
         if (g.slices > 1) {
-          if (m < g.M) {
-            if (g.rsync)  // write-through (sc1): another workgroup of the range adds it up
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j]), prs,
-                                                     (int)((((int64_t)slice * g.M + m) * N16 + n0) * 4), 0, 16);
-            else *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = acc[j];
-          }
+          if (m < g.M) store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, acc[j]);
         } else if (m < g.M) {
           const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
 #pragma unroll
@@ -1948,58 +2009,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   wait_vmcnt<0>();
   LK_PTRACE(6);
 #undef LK_PTRACE
-  if (g.rsync) {
-    // fused split-K reduction: every wave's slab stores have completed (write-through); one lane
-    // arrives on the range's counter and waits for the range's other slices (all tasks are
-    // co-resident: the host launches at most one per CU), then the workgroup adds its share of
-    // the range's rows, slabs in slice order (as splitk_reduce_kernel: bit-identical)
-    __builtin_amdgcn_s_barrier();
-    if (wave == 0 && lane == 0) {
-      unsigned *c = g.rsync + range * kChainLine;
-      const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned target = (old / (unsigned)g.slices + 1u) * (unsigned)g.slices;
-      const uint64_t ts = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - ts > 20000000ull) {  // 200 ms: flag, run on, never hang
-          __hip_atomic_store(g.rsync + (int64_t)gridDim.x * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    asm volatile("" ::: "memory");  // the slab loads stay after the poll
-    __builtin_amdgcn_s_barrier();
-    const int m0 = t0 * 16, m1 = min(t1 * 16, g.M);
-    const int per = (m1 - m0 + g.slices - 1) / g.slices;
-    const int r0 = min(m0 + slice * per, m1), r1 = min(r0 + per, m1);
-    const int c4 = N16 / 4;
-    for (int idx = (int)threadIdx.x; idx < (r1 - r0) * c4; idx += NW * 64) {
-      const int64_t m = r0 + idx / c4;
-      const int n0 = (idx % c4) * 4;
-      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-      for (int b = 0; b < g.slices; b += 8) {
-        f32x4 v[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-          if (b + i < g.slices)
-            v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)(b + i) * g.M + m) * N16 + n0) * 4), 0, 16));
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-          if (b + i < g.slices) {
-            if (b + i == 0) sum = v[i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
-            else { sum.x += v[i].x; sum.y += v[i].y; sum.z += v[i].z; sum.w += v[i].w; }
-          }
-      }
-      const float e4[4] = {sum.x, sum.y, sum.z, sum.w};
-      if (g.d_nb0 == 4 && n0 + 4 <= g.N && (((uintptr_t)(g.dst + m * g.d_nb1 + n0 * 4)) & 15) == 0) {
-        *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = sum;
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-          if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
-      }
-    }
-  }
+  if (g.rsync)
+    splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, g.dst, g.d_nb0,
+                            g.d_nb1, wave, lane);
 }
 
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------

@@ -78,6 +78,7 @@ struct SkArgs {
   float *partial;          // [slices][M][16·NT] when slices > 1
   int32_t M, N, K;
   int32_t slices, tiles_per_range, tasks;  // tasks = ranges·slices (the grid is padded to 8)
+  unsigned *rsync;         // gemm_sk_kernel: fused split-K reduction (SkinnyArgs::rsync), or null
 };
 
 // LDS-typed pointers throughout (no generic -> LDS conversions, no null checks on them).
@@ -417,6 +418,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   LK_SKT(1, __builtin_amdgcn_s_memrealtime());
 
   const int N16 = 16 * NT;
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
   // h = 0 collects unit u − 1's partner sums after computing unit u (the partner, at higher issue
   // priority, is ahead), so neither wave idles while the other computes: the two waves of a SIMD
   // overlap their VALU / MFMA streams.
@@ -438,7 +441,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     for (int j = 0; j < NT; j++) {
       const int n0 = 16 * j + 4 * (lane >> 4);
       if (g.slices > 1) {
-        if (m < g.M) *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = sum[j];
+        if (m < g.M) store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, sum[j]);
       } else if (m < g.M) {
         const float e4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
 #pragma unroll
@@ -560,6 +563,9 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   LK_SKT(6, c_comp);
   LK_SKT(7, c_hand);
   wait_vmcnt<0>();
+  if (g.rsync)
+    splitk_fused_reduce<G::NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, g.dst, g.d_nb0,
+                               g.d_nb1, wave, lane);
 }
 
 // ---- one wave per SIMD: 16 blocks per wave, no hand-off ----------------------------------------
