@@ -801,9 +801,13 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
   const int nsuper = ((g.tiles_m + g.sm - 1) / g.sm) * ((g.tiles_n + g.sn - 1) / g.sn);
   g.tasks = nsuper * g.sm * g.sn * slices;
   const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
+  static const int w2 = [] { const char *e = getenv("LK_WIDE2"); return e ? atoi(e) : 0; }();
+  // fused split-K reduction in gemm_wide_kernel when every task is co-resident (one per CU)
+  g.rsync = nullptr;
+  if (!w2 && g.tasks <= cu_count())
+    if (int rf = fused_rsync(slices, (size_t)slices * g.M * npad * sizeof(float), &g.rsync)) return rf;
   // LK_WIDE2=1 / 2: gemm_wide2_kernel (lk_wide2.hpp, dedicated loader waves, 4 / 8 consumers) on the same tiles; its
   // Q4 codes are 128 + n, so the activations come in xsplit's q4_order 2 with T = MULT·Σ(hi + lo)
-  static const int w2 = [] { const char *e = getenv("LK_WIDE2"); return e ? atoi(e) : 0; }();
   XSplitArgs xw = xa;
   if (w2 && QT != LK_TYPE_Q8_0) {
     xw.q4_order = 2;
@@ -819,7 +823,7 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
     hipLaunchKernelGGL((gemm_wide2_kernel<QT, 4>), dim3(grid), dim3(G4::NW * 64), G4::LDS, st, g);
   }
   else hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
-  if (slices > 1) {
+  if (slices > 1 && !g.rsync) {
     const int64_t threads = (int64_t)g.M * (npad / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
                        slices, g.M, g.N, npad, g.dst, g.d_nb0, g.d_nb1);

@@ -1598,10 +1598,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
 // the result is bit-identical to it. rsync: the counter row of this `slices` value (each call adds
 // exactly `slices` per range, so every counter is a multiple of slices between calls); the word
 // gridDim.x lines on is a timeout flag (a 200 ms bound instead of a hang).
+// Slab rows are N16 floats apart; the range covers columns [n_lo, n_lo + n_cnt) (n_cnt % 4 == 0).
 template <int NW>
 __device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amdgpu_buffer_rsrc_t prs, int range, int slice,
-                                                    int slices, int m0, int m1, int M, int N, int N16, uint8_t *dst,
-                                                    int64_t d_nb0, int64_t d_nb1, int wave, int lane) {
+                                                    int slices, int m0, int m1, int M, int N, int N16, int n_lo, int n_cnt,
+                                                    uint8_t *dst, int64_t d_nb0, int64_t d_nb1, int wave, int lane) {
   __builtin_amdgcn_s_barrier();
   if (wave == 0 && lane == 0) {
     unsigned *c = rsync + range * kChainLine;
@@ -1620,10 +1621,10 @@ __device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amd
   __builtin_amdgcn_s_barrier();
   const int per = (m1 - m0 + slices - 1) / slices;
   const int r0 = min(m0 + slice * per, m1), r1 = min(r0 + per, m1);
-  const int c4 = N16 / 4;
+  const int c4 = n_cnt / 4;
   for (int idx = (int)threadIdx.x; idx < (r1 - r0) * c4; idx += NW * 64) {
     const int64_t m = r0 + idx / c4;
-    const int n0 = (idx % c4) * 4;
+    const int n0 = n_lo + (idx % c4) * 4;
     f32x4 sum = {0.f, 0.f, 0.f, 0.f};
     for (int b = 0; b < slices; b += 8) {
       f32x4 v[8];
@@ -2010,8 +2011,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   LK_PTRACE(6);
 #undef LK_PTRACE
   if (g.rsync)
-    splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, g.dst, g.d_nb0,
-                            g.d_nb1, wave, lane);
+    splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
+                            g.d_nb0, g.d_nb1, wave, lane);
 }
 
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------
@@ -2073,6 +2074,7 @@ struct WideArgs {
   int32_t tiles_m, tiles_n, slices, kslice;  // kslice: blocks per slice (a multiple of SB)
   int32_t tasks;                             // task space: super-tiles x sm·sn·slices (grid padded to 8)
   int32_t sm, sn;                            // super-tile: sm row bands x sn column tiles
+  unsigned *rsync;                           // fused split-K reduction per output tile, or null
 };
 
 template <int QT>
@@ -2272,7 +2274,10 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
       for (int j = 0; j < NT; j++) red[(i * NT + j) * 64] = acc[i][j];
   }
   __syncthreads();
-  if (kg != 0) return;
+  const int npad = g.tiles_n * BN;
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * npad * 4 : 0, 0x00020000);
+  if (kg == 0) {
 #pragma unroll
   for (int i = 0; i < MT; i++)
 #pragma unroll
@@ -2281,7 +2286,6 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
       acc[i][j].x += o.x; acc[i][j].y += o.y; acc[i][j].z += o.z; acc[i][j].w += o.w;
     }
   // outputs: lane holds C'(n = 16·(tn·NT + j) + 4(lane>>4) + e, m = tm·BM + (mw·MT + i)·16 + (lane&15))
-  const int npad = g.tiles_n * BN;
 #pragma unroll
   for (int i = 0; i < MT; i++) {
     const int64_t m = (int64_t)tm * BM + (mw * MT + i) * 16 + (lane & 15);
@@ -2290,7 +2294,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
     for (int j = 0; j < NT; j++) {
       const int n0 = tn * BN + j * 16 + 4 * (lane >> 4);
       if (g.slices > 1) {
-        *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * npad + n0)) = acc[i][j];
+        store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * npad + n0, acc[i][j]);
       } else {
         const float e4[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
         if (g.d_nb0 == 4 && n0 + 4 <= g.N && ((((uintptr_t)g.dst + m * g.d_nb1 + n0 * 4) & 15) == 0)) {
@@ -2302,6 +2306,12 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
         }
       }
     }
+  }
+  }
+  if (g.rsync) {  // every wave (both K-groups) joins: the tile's slices add up its rows
+    wait_vmcnt<0>();
+    splitk_fused_reduce<8>(g.rsync, prs, tm * g.tiles_n + tn, slice, g.slices, tm * BM, min(tm * BM + BM, g.M), g.M, g.N, npad,
+                           tn * BN, BN, g.dst, g.d_nb0, g.d_nb1, wave, lane);
   }
 }
 

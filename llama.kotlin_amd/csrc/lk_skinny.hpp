@@ -564,8 +564,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   LK_SKT(7, c_hand);
   wait_vmcnt<0>();
   if (g.rsync)
-    splitk_fused_reduce<G::NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, g.dst, g.d_nb0,
-                               g.d_nb1, wave, lane);
+    splitk_fused_reduce<G::NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
+                               g.d_nb0, g.d_nb1, wave, lane);
 }
 
 // ---- one wave per SIMD: 16 blocks per wave, no hand-off ----------------------------------------
