@@ -562,7 +562,7 @@ def next_rows(torch, G, dev, reps=20):
         nbytes = nb + 4 * K * N + 4 * M * N
         out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
                      "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
-                     "kernel": "kquant_n1_kernel" if N == 1 else ("gemm_sk_kernel<Q4_K> (xsplit + wave-pair MFMA + splitk_reduce)" if 16 <= N <= 32 and qn == "Q4_K" else "kquant_nc_kernel"),
+                     "kernel": "kquant_n1_kernel" if N == 1 else ("gemm_sk_kernel<Q4_K> (wave-pair MFMA; activation split and split-K reduction in the kernel)" if 16 <= N <= 32 and qn == "Q4_K" else "kquant_nc_kernel"),
                      "rotating_weight_copies": copies, "hip_graph": graphed}
         del g
     # format kernels: dequantize / quantize of a Q4_0 11008 x 4096 matrix

@@ -542,8 +542,12 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
   const int nblk = g.K / 32;
   const int slices = (nblk + SG::SB - 1) / SG::SB;
   const int ntile = (g.M + 15) / 16;
-  // one workgroup per CU (LDS): about cu_count() workgroups in all
-  int ranges = std::max(1, std::min(ntile, (cu_count() + slices - 1) / slices));
+  // one workgroup per CU (LDS): about cu_count() workgroups in all; fused split-K reduction
+  // unless LK_SKP_UNFUSED=1 (every task co-resident)
+  const int cu = cu_count();
+  unsigned *rsync = nullptr;
+  if (int rf = fused_rsync(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), &rsync)) return rf;
+  int ranges = std::max(1, std::min(ntile, rsync ? cu / slices : (cu + slices - 1) / slices));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   g.slices = slices;
@@ -553,9 +557,10 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
     g.partial = (float *)S.partial;
   }
   g.tasks = ranges * slices;
+  g.rsync = rsync;
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_skinny_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
-  if (slices > 1) {
+  if (slices > 1 && !rsync) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
                        slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);

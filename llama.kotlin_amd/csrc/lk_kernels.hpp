@@ -1411,6 +1411,73 @@ __device__ __forceinline__ void skinny_blocks(const uint32_t (&w)[SB][WPB], cons
   }
 }
 
+// Fused split-K reduction (the skinny kernels, gemm_sk_kernel, gemm_wide_kernel): called by every wave of a
+// task once its partial slab rows [m0, m1) of slice `slice` are stored write-through (sc1) and
+// drained. One lane arrives on the row range's counter and waits for the range's other slices (the
+// host launches every task co-resident: at most one workgroup per CU), then the workgroup adds its
+// 1/slices share of the range's rows, slabs in slice order — the order of splitk_reduce_kernel, so
+// the result is bit-identical to it. rsync: the counter row of this `slices` value (each call adds
+// exactly `slices` per range, so every counter is a multiple of slices between calls); the word
+// gridDim.x lines on is a timeout flag (a 200 ms bound instead of a hang).
+// Slab rows are N16 floats apart; the range covers columns [n_lo, n_lo + n_cnt) (n_cnt % 4 == 0).
+template <int NW>
+__device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amdgpu_buffer_rsrc_t prs, int range, int slice,
+                                                    int slices, int m0, int m1, int M, int N, int N16, int n_lo, int n_cnt,
+                                                    uint8_t *dst, int64_t d_nb0, int64_t d_nb1, int wave, int lane) {
+  __builtin_amdgcn_s_barrier();
+  if (wave == 0 && lane == 0) {
+    unsigned *c = rsync + range * kChainLine;
+    const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (old / (unsigned)slices + 1u) * (unsigned)slices;
+    const uint64_t ts = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - ts > 20000000ull) {  // 200 ms at 100 MHz
+        __hip_atomic_store(rsync + (int64_t)gridDim.x * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  asm volatile("" ::: "memory");  // the slab loads stay after the poll
+  __builtin_amdgcn_s_barrier();
+  const int per = (m1 - m0 + slices - 1) / slices;
+  const int r0 = min(m0 + slice * per, m1), r1 = min(r0 + per, m1);
+  const int c4 = n_cnt / 4;
+  for (int idx = (int)threadIdx.x; idx < (r1 - r0) * c4; idx += NW * 64) {
+    const int64_t m = r0 + idx / c4;
+    const int n0 = n_lo + (idx % c4) * 4;
+    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < slices; b += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if (b + i < slices)
+          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)(b + i) * M + m) * N16 + n0) * 4), 0, 16));
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if (b + i < slices) {
+          if (b + i == 0) sum = v[i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
+          else { sum.x += v[i].x; sum.y += v[i].y; sum.z += v[i].z; sum.w += v[i].w; }
+        }
+    }
+    const float e4[4] = {sum.x, sum.y, sum.z, sum.w};
+    if (d_nb0 == 4 && n0 + 4 <= N && (((uintptr_t)(dst + m * d_nb1 + n0 * 4)) & 15) == 0) {
+      *(f32x4 *)(dst + m * d_nb1 + n0 * 4) = sum;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (n0 + q < N) *(float *)(dst + m * d_nb1 + (n0 + q) * d_nb0) = e4[q];
+    }
+  }
+}
+
+// a partial slab's f32x4: write-through when the reduction is fused (another workgroup reads it)
+__device__ __forceinline__ void store_partial(bool fused, const __amdgpu_buffer_rsrc_t prs, float *partial, int64_t idx,
+                                              f32x4 v) {
+  if (fused) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), prs, (int)(idx * 4), 0, 16);
+  else *(f32x4 *)(partial + idx) = v;
+}
+
 #ifdef LK_SKINNY_TRACE
 __device__ uint64_t *lk_strace_buf;
 #endif
@@ -1542,6 +1609,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
     }
 
   const int N16 = 16 * NT;
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
   int slot = 0;
   for (int u = 0; u < nunits; u++) {
     // ops younger than unit u's DMA (issue order: units 0..D-1 in the prologue, then per tile
@@ -1574,7 +1643,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
     for (int j = 0; j < NT; j++) {
       const int n0 = 16 * j + 4 * (lane >> 4);
       if (g.slices > 1) {
-        if (m < g.M) *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = acc[j];
+        if (m < g.M) store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, acc[j]);
       } else if (m < g.M) {
         const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
 #pragma unroll
@@ -1588,73 +1657,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
   wait_vmcnt<0>();
   LK_STRACE(6);
 #undef LK_STRACE
-}
-
-// Fused split-K reduction (gemm_skinny_pair_kernel, gemm_sk_kernel): called by every wave of a
-// task once its partial slab rows [m0, m1) of slice `slice` are stored write-through (sc1) and
-// drained. One lane arrives on the row range's counter and waits for the range's other slices (the
-// host launches every task co-resident: at most one workgroup per CU), then the workgroup adds its
-// 1/slices share of the range's rows, slabs in slice order — the order of splitk_reduce_kernel, so
-// the result is bit-identical to it. rsync: the counter row of this `slices` value (each call adds
-// exactly `slices` per range, so every counter is a multiple of slices between calls); the word
-// gridDim.x lines on is a timeout flag (a 200 ms bound instead of a hang).
-// Slab rows are N16 floats apart; the range covers columns [n_lo, n_lo + n_cnt) (n_cnt % 4 == 0).
-template <int NW>
-__device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amdgpu_buffer_rsrc_t prs, int range, int slice,
-                                                    int slices, int m0, int m1, int M, int N, int N16, int n_lo, int n_cnt,
-                                                    uint8_t *dst, int64_t d_nb0, int64_t d_nb1, int wave, int lane) {
-  __builtin_amdgcn_s_barrier();
-  if (wave == 0 && lane == 0) {
-    unsigned *c = rsync + range * kChainLine;
-    const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = (old / (unsigned)slices + 1u) * (unsigned)slices;
-    const uint64_t ts = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - ts > 20000000ull) {  // 200 ms at 100 MHz
-        __hip_atomic_store(rsync + (int64_t)gridDim.x * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  asm volatile("" ::: "memory");  // the slab loads stay after the poll
-  __builtin_amdgcn_s_barrier();
-  const int per = (m1 - m0 + slices - 1) / slices;
-  const int r0 = min(m0 + slice * per, m1), r1 = min(r0 + per, m1);
-  const int c4 = n_cnt / 4;
-  for (int idx = (int)threadIdx.x; idx < (r1 - r0) * c4; idx += NW * 64) {
-    const int64_t m = r0 + idx / c4;
-    const int n0 = n_lo + (idx % c4) * 4;
-    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < slices; b += 8) {
-      f32x4 v[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++)
-        if (b + i < slices)
-          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)(b + i) * M + m) * N16 + n0) * 4), 0, 16));
-#pragma unroll
-      for (int i = 0; i < 8; i++)
-        if (b + i < slices) {
-          if (b + i == 0) sum = v[i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
-          else { sum.x += v[i].x; sum.y += v[i].y; sum.z += v[i].z; sum.w += v[i].w; }
-        }
-    }
-    const float e4[4] = {sum.x, sum.y, sum.z, sum.w};
-    if (d_nb0 == 4 && n0 + 4 <= N && (((uintptr_t)(dst + m * d_nb1 + n0 * 4)) & 15) == 0) {
-      *(f32x4 *)(dst + m * d_nb1 + n0 * 4) = sum;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (n0 + q < N) *(float *)(dst + m * d_nb1 + (n0 + q) * d_nb0) = e4[q];
-    }
-  }
-}
-
-// a partial slab's f32x4: write-through when the reduction is fused (another workgroup reads it)
-__device__ __forceinline__ void store_partial(bool fused, const __amdgpu_buffer_rsrc_t prs, float *partial, int64_t idx,
-                                              f32x4 v) {
-  if (fused) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), prs, (int)(idx * 4), 0, 16);
-  else *(f32x4 *)(partial + idx) = v;
+  if (g.rsync)
+    splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
+                            g.d_nb0, g.d_nb1, wave, lane);
 }
 
 // ---- skinny GEMM on wave pairs (Q4_0 / Q4_1, 17 <= N <= 32) -------------------------------
