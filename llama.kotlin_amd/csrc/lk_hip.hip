@@ -818,7 +818,8 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
     xw.q4_order = 2;
     xw.mult = Wide2Geom<QT>::MULT;
   }
-  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xw);
+  static const bool skip_xsplit = getenv("LK_LAB_SKIP_XSPLIT") != nullptr;  // lab (wrong results): the split's share
+  if (!skip_xsplit) hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xw);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   if (w2 == 2) {
     using G8 = Wide2Geom<QT, 8>;
