@@ -180,9 +180,9 @@ int lk_plan_launch(lk_plan *plan, void *stream);
 int lk_plan_num_launches(const lk_plan *plan);
 /* A chain of DEPENDENT stages in one launch (a persistent streaming GEMV): node i belongs to
  * stage stage[i] (0, then non-decreasing by at most 1). Stage s+1 starts only after every
- * node of stage s has stored its outputs — a device-side grid barrier (agent-scope release /
- * acquire) — so a stage may read what the previous one wrote; the next stage's weights are
- * already streaming while the barrier completes. Same results as launching the stages' plans
+ * node of stage s has stored its outputs — a device-side grid barrier (write-through outputs,
+ * sharded arrival counters, activations re-read past the caches) — so a stage may read what the
+ * previous one wrote; the next stage's weights are already streaming while the barrier completes. Same results as launching the stages' plans
  * in order. Every node must be an N = 1 streaming-GEMV node of one quant type
  * (LK_ERR_NOT_IMPLEMENTED otherwise). Launch with lk_plan_launch (graph-capturable). */
 int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage, int n,
@@ -191,6 +191,12 @@ int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor
  * then undefined) and re-arms the plan; 0 otherwise. Synchronizes the device. */
 int lk_plan_chain_timed_out(lk_plan *plan);
 void lk_plan_destroy(lk_plan *plan);
+/* Batched MUL_MATs (2 <= N) reduce their K slices inside the launch, workgroups waiting for each
+ * other (every workgroup co-resident: at most one per CU). *count = how many of those waits on
+ * the current device gave up at their 200 ms bound since the last call (the results of those
+ * launches are undefined; never seen with one process per GPU), then resets the count.
+ * Synchronizes the device. Diagnostic; no reference counterpart. */
+int lk_sync_timeouts(uint32_t *count);
 
 /* ---- multi-GPU: row shards + RCCL all-gather over xGMI -----------------
  * The reference is single-device; this is the north star's partition of the same operator.

@@ -1696,6 +1696,20 @@ int lk_plan_chain_timed_out(lk_plan *plan) {
   return 0;
 }
 
+int lk_sync_timeouts(uint32_t *count) {
+  if (!count) return fail(LK_ERR_INVALID_ARG, "null count");
+  int rc = ensure_init();
+  if (rc) return rc;
+  unsigned v = 0;
+  const unsigned zero = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(LK_ERR_DEVICE, "sync");
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(lk_sync_timeout_count), sizeof(v)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(lk_sync_timeout_count), &zero, sizeof(zero)) != hipSuccess)
+    return fail(LK_ERR_DEVICE, "timeout count");
+  *count = v;
+  return LK_OK;
+}
+
 int lk_plan_launch(lk_plan *plan, void *stream) {
   if (!plan) return fail(LK_ERR_INVALID_ARG, "null plan");
   hipStream_t st = pick_stream(stream);

@@ -1411,14 +1411,17 @@ __device__ __forceinline__ void skinny_blocks(const uint32_t (&w)[SB][WPB], cons
   }
 }
 
+// Waits that gave up at their bound (fused split-K reductions), read and reset by lk_sync_timeouts.
+__device__ unsigned lk_sync_timeout_count;
+
 // Fused split-K reduction (the skinny kernels, gemm_sk_kernel, gemm_wide_kernel): called by every wave of a
 // task once its partial slab rows [m0, m1) of slice `slice` are stored write-through (sc1) and
 // drained. One lane arrives on the row range's counter and waits for the range's other slices (the
 // host launches every task co-resident: at most one workgroup per CU), then the workgroup adds its
 // 1/slices share of the range's rows, slabs in slice order — the order of splitk_reduce_kernel, so
 // the result is bit-identical to it. rsync: the counter row of this `slices` value (each call adds
-// exactly `slices` per range, so every counter is a multiple of slices between calls); the word
-// gridDim.x lines on is a timeout flag (a 200 ms bound instead of a hang).
+// exactly `slices` per range, so every counter is a multiple of slices between calls); a wait
+// past 200 ms counts itself in lk_sync_timeout_count and runs on instead of hanging.
 // Slab rows are N16 floats apart; the range covers columns [n_lo, n_lo + n_cnt) (n_cnt % 4 == 0).
 template <int NW>
 __device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amdgpu_buffer_rsrc_t prs, int range, int slice,
@@ -1432,8 +1435,8 @@ __device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amd
     const uint64_t ts = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - ts > 20000000ull) {  // 200 ms at 100 MHz
-        __hip_atomic_store(rsync + (int64_t)gridDim.x * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_s_memrealtime() - ts > 20000000ull) {  // 200 ms at 100 MHz: count it, run on
+        __hip_atomic_fetch_add(&lk_sync_timeout_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }

@@ -75,7 +75,7 @@ EXPORTED_SYMBOLS = (
     "lk_init", "lk_device_count", "lk_last_error", "lk_shutdown", "lk_version",
     "lk_mul_mat_validate", "lk_mul_mat", "lk_mul_mat_device", "lk_mul_mat_sharded", "lk_weights_pin_sharded",
     "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy", "lk_plan_create_chain",
-    "lk_plan_chain_timed_out",
+    "lk_plan_chain_timed_out", "lk_sync_timeouts",
     "lk_graph_create", "lk_graph_compute", "lk_graph_num_levels", "lk_graph_num_launches",
     "lk_graph_transfer_bytes", "lk_graph_destroy", "lk_graph_num_rebinds",
     "lk_weights_pin", "lk_weights_evict", "lk_weights_evict_buffer", "lk_weights_evict_all",
@@ -125,6 +125,7 @@ def load():
     L.lk_plan_launch.argtypes = [vp, vp]
     L.lk_plan_create_chain.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.POINTER(vp)]
     L.lk_plan_chain_timed_out.argtypes = [vp]
+    L.lk_sync_timeouts.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
     L.lk_plan_num_launches.argtypes = [vp]
     L.lk_plan_destroy.argtypes = [vp]
     L.lk_plan_destroy.restype = None

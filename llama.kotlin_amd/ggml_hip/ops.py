@@ -338,9 +338,17 @@ def weightsPinSharded(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, nShards
     _lib.check(_lib.load().lk_weights_pin_sharded(ctypes.byref(to_lk(graphAllocator, a)), generation, int(nShards)))
 
 
+def syncTimeouts() -> int:
+    """In-kernel waits of the batched kernels' fused split-K reduction that gave up at their bound
+    since the last call (lk_sync_timeouts; synchronizes the device, resets the count)."""
+    n = ctypes.c_uint32(0)
+    _lib.check(_lib.load().lk_sync_timeouts(ctypes.byref(n)))
+    return int(n.value)
+
+
 def weightsEvictAll():
     _lib.load().lk_weights_evict_all()
 
 
-__all__ = ["computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+__all__ = ["syncTimeouts", "computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
            "weightsEvictAll", "weightsEvict", "weightsEvictBuffer", "weightsCachedBytes", "weightsCachedCount", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]

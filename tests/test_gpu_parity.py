@@ -451,3 +451,14 @@ def test_q32_gemm_vs_oracle(gpu, oracle, qt, shape, monkeypatch):
         assert ok, (kind, msg)
         again = gpu_matmul(qt, q, M, K, N, x)
         assert np.array_equal(got.view(np.uint32), again.view(np.uint32)), "not deterministic"
+
+
+def test_no_sync_timeouts(gpu, oracle):
+    """The batched kernels' in-launch split-K reduction (every workgroup co-resident, waits bounded
+    at 200 ms): after a C3-shaped skinny call, a 22-slice skinny call and a C5-shaped wide call,
+    and every batched test before this one, no wait has given up (lk_sync_timeouts)."""
+    import ggml_hip as G
+    for (qt, M, K, N) in [(2, 11008, 4096, 32), (2, 4096, 11008, 32), (2, 4096, 4096, 64), (3, 1000, 4096, 8)]:
+        q, x = make_inputs(oracle, qt, M, K, N, "random", seed=M + N)
+        gpu_matmul(qt, q, M, K, N, x)
+    assert G.syncTimeouts() == 0
