@@ -2775,6 +2775,39 @@ __device__ __forceinline__ float kq32_dot(const Kq32Raw<QT> &r, int s, const KqT
   return a;
 }
 
+// Q4_K at batch 1, factored: Σ_e w_e·x_e with w_e = (q_e/15)·scale + off (:297-306) computed as
+// (Σ q_e·x_e)/15·scale + off·Σ x_e: the codes enter as exact fp8 conversions (n·2⁻⁹, two per
+// v_cvt_pk_f32_fp8) against the activations in nibble order (x0,x2,x4,x6 | x1,x3,x5,x7 per 8,
+// as the stream kernel holds them), Σx comes from the pad slot 32 of the sub-block's LDS row. The
+// quotient is correctly rounded (__fdiv_rn) and nothing is contracted, so a one-hot activation
+// still yields the Kotlin weight bit for bit (S_q = q, Σx = 1, the other lanes exact zeros); in
+// general only the f32 summation order differs from the reference, as everywhere else.
+__device__ __forceinline__ float kq32_dot_q4k_factored(const Kq32Raw<LK_TYPE_Q4_K> &r, int s, const KqTables &t,
+                                                       const f32x4 *xv, float a) {
+#pragma clang fp contract(off)
+  const float d = h2f(r.h.x & 0xFFFF), dmin = h2f(r.h.x >> 16);
+  const int sc = sext8(byte_of(r.h, 4 + s));
+  const int qmh = (s * 2 + 1 < LK_K_SCALE_SIZE) ? (sext8(byte_of(r.h, 5 + 2 * s)) & 0x0F) : 0;
+  const int qm = ((sc >> 6) & 0x03) | (qmh << 2);
+  const float scale = t.q63[sc & 0x3F] * d;
+  const float off = t.q63[qm] * d + dmin;
+  const uint32_t cw[4] = {r.c.x, r.c.y, r.c.z, r.c.w};
+  f2v s2 = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t lo = cw[j] & 0x0F0F0F0Fu, hi = (cw[j] >> 4) & 0x0F0F0F0Fu;
+    const f32x4 xa = xv[2 * j], xb = xv[2 * j + 1];
+    s2 = __builtin_elementwise_fma(fp8x2<false>(lo), f2v{xa.x, xa.y}, s2);
+    s2 = __builtin_elementwise_fma(fp8x2<true>(lo), f2v{xa.z, xa.w}, s2);
+    s2 = __builtin_elementwise_fma(fp8x2<false>(hi), f2v{xb.x, xb.y}, s2);
+    s2 = __builtin_elementwise_fma(fp8x2<true>(hi), f2v{xb.z, xb.w}, s2);
+  }
+  const float sq = (s2.x + s2.y) * 512.f;             // Σ q·x (the 2⁻⁹ scaling is exact)
+  const float sx = ((const float *)xv)[32];            // Σ x of the sub-block
+  const float part = __fdiv_rn(sq, 15.0f) * scale;
+  return a + (part + off * sx);
+}
+
 template <int QT, int ROWS>  // rows (waves) per workgroup
 __global__ __launch_bounds__(ROWS * 64) void kquant_n1_kernel(KQuantArgs g) {
   constexpr int BB = KQTraits<QT>::BB, U = 2;
@@ -2784,7 +2817,20 @@ __global__ __launch_bounds__(ROWS * 64) void kquant_n1_kernel(KQuantArgs g) {
   if (tid < 64) t.q63[tid] = __fdiv_rn((float)tid, 63.0f);
   else if (tid < 80) t.q15[tid - 64] = __fdiv_rn((float)(tid - 64), 15.0f);
   else if (tid < 84) t.q3[tid - 80] = __fdiv_rn((float)(tid - 80), 3.0f);
-  for (int64_t k = tid; k < g.K; k += ROWS * 64) xs[(k >> 5) * 36 + (k & 31)] = *(const float *)(g.b + k * g.b_nb1);
+  if constexpr (QT == LK_TYPE_Q4_K) {  // nibble order within each 8, then Σx per 32 in the pad
+    for (int64_t k = tid; k < g.K; k += ROWS * 64)
+      xs[(k >> 5) * 36 + (k & 24) + ((k & 1) ? 4 : 0) + ((k & 7) >> 1)] = *(const float *)(g.b + k * g.b_nb1);
+    __syncthreads();
+    for (int64_t sbk = tid; sbk < g.K / 32; sbk += ROWS * 64) {
+      const f32x4 *v = (const f32x4 *)(xs + sbk * 36);
+      f32x4 a4 = v[0];
+#pragma unroll
+      for (int j = 1; j < 8; j++) a4 += v[j];
+      xs[sbk * 36 + 32] = (a4.x + a4.y) + (a4.z + a4.w);
+    }
+  } else {
+    for (int64_t k = tid; k < g.K; k += ROWS * 64) xs[(k >> 5) * 36 + (k & 31)] = *(const float *)(g.b + k * g.b_nb1);
+  }
   __syncthreads();
   const int lane = tid & 63;
   const int64_t i = (int64_t)blockIdx.x * ROWS + __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2801,7 +2847,10 @@ __global__ __launch_bounds__(ROWS * 64) void kquant_n1_kernel(KQuantArgs g) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int64_t blk = (c0 + u) * 8 + (lane >> 3);
-      const float a = kq32_dot<QT>(r[u], s, t, (const f32x4 *)(xs + (min(blk, nb - 1) * 8 + s) * 36), acc);
+      const f32x4 *xv = (const f32x4 *)(xs + (min(blk, nb - 1) * 8 + s) * 36);
+      float a;
+      if constexpr (QT == LK_TYPE_Q4_K) a = kq32_dot_q4k_factored(r[u], s, t, xv, acc);
+      else a = kq32_dot<QT>(r[u], s, t, xv, acc);
       acc = blk < nb ? a : acc;
     }
   }
