@@ -2808,6 +2808,55 @@ __device__ __forceinline__ float kq32_dot_q4k_factored(const Kq32Raw<LK_TYPE_Q4_
   return a + (part + off * sx);
 }
 
+// Q2_K at batch 1, factored the same way per 16-item sub-block (:182-196): (Σ q·x)/3·scale +
+// min·Σx, the 2-bit codes as fp8 conversions against activations ordered (x0,x4,x8,x12 | x1,x5,..)
+// per 16; Σx of the two halves in pad slots 32 and 33.
+__device__ __forceinline__ float kq32_dot_q2k_factored(const Kq32Raw<LK_TYPE_Q2_K> &r, const KqTables &t, const f32x4 *xv,
+                                                       float a) {
+#pragma clang fp contract(off)
+  const float d = h2f(r.h & 0xFFFF), dmin = h2f(r.h >> 16);
+#pragma unroll
+  for (int hsb = 0; hsb < 2; hsb++) {
+    const int sm = sext8((r.sc >> (8 * hsb)) & 0xFF);
+    const float scale = t.q15[sm & 0x0F] * d;
+    const float mn = (float)((sm >> 4) & 0x0F) * d + dmin;
+    const uint32_t cw = hsb ? r.c1 : r.c0;
+    f2v s2 = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // bit pair j of each byte: items j, 4 + j, 8 + j, 12 + j
+      const uint32_t b = (cw >> (2 * j)) & 0x03030303u;
+      const f32x4 xa = xv[4 * hsb + j];
+      s2 = __builtin_elementwise_fma(fp8x2<false>(b), f2v{xa.x, xa.y}, s2);
+      s2 = __builtin_elementwise_fma(fp8x2<true>(b), f2v{xa.z, xa.w}, s2);
+    }
+    const float sq = (s2.x + s2.y) * 512.f;
+    const float sx = ((const float *)xv)[32 + hsb];
+    a = a + (__fdiv_rn(sq, 3.0f) * scale + mn * sx);
+  }
+  return a;
+}
+
+// Q8_K at batch 1, factored (:404-407): (Σ (q + 128)·x − 128·Σx)·d, the biased bytes converted
+// exactly by v_cvt_f32_ubyteN; Σx in pad slot 32. One-hot: (q + 128) − 128 = q, times d: the
+// Kotlin weight q·d bit for bit.
+__device__ __forceinline__ float kq32_dot_q8k_factored(const Kq32Raw<LK_TYPE_Q8_K> &r, const f32x4 *xv, float a) {
+#pragma clang fp contract(off)
+  const float d = __builtin_bit_cast(float, r.d);
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint32_t u = r.c[j] ^ 0x80808080u;
+    const f32x4 x = xv[j];
+    s1 = fmaf((float)(u & 0xFF), x.x, s1);  // v_cvt_f32_ubyteN
+    s2 = fmaf((float)((u >> 8) & 0xFF), x.y, s2);
+    s1 = fmaf((float)((u >> 16) & 0xFF), x.z, s1);
+    s2 = fmaf((float)(u >> 24), x.w, s2);
+  }
+  const float sx = ((const float *)xv)[32];
+  const float sq = (s1 + s2) - 128.f * sx;
+  return a + sq * d;
+}
+
 template <int QT, int ROWS>  // rows (waves) per workgroup
 __global__ __launch_bounds__(ROWS * 64) void kquant_n1_kernel(KQuantArgs g) {
   constexpr int BB = KQTraits<QT>::BB, U = 2;
@@ -2817,19 +2866,26 @@ __global__ __launch_bounds__(ROWS * 64) void kquant_n1_kernel(KQuantArgs g) {
   if (tid < 64) t.q63[tid] = __fdiv_rn((float)tid, 63.0f);
   else if (tid < 80) t.q15[tid - 64] = __fdiv_rn((float)(tid - 64), 15.0f);
   else if (tid < 84) t.q3[tid - 80] = __fdiv_rn((float)(tid - 80), 3.0f);
-  if constexpr (QT == LK_TYPE_Q4_K) {  // nibble order within each 8, then Σx per 32 in the pad
-    for (int64_t k = tid; k < g.K; k += ROWS * 64)
-      xs[(k >> 5) * 36 + (k & 24) + ((k & 1) ? 4 : 0) + ((k & 7) >> 1)] = *(const float *)(g.b + k * g.b_nb1);
-    __syncthreads();
-    for (int64_t sbk = tid; sbk < g.K / 32; sbk += ROWS * 64) {
-      const f32x4 *v = (const f32x4 *)(xs + sbk * 36);
-      f32x4 a4 = v[0];
-#pragma unroll
-      for (int j = 1; j < 8; j++) a4 += v[j];
-      xs[sbk * 36 + 32] = (a4.x + a4.y) + (a4.z + a4.w);
+  // the factored dots' activation order within each 32 (Q4_K: nibble order per 8; Q2_K: bit-pair
+  // order per 16; Q8_K: natural), then Σx in the pad: per 32 (Q4_K, Q8_K) or per 16 (Q2_K)
+  for (int64_t k = tid; k < g.K; k += ROWS * 64) {
+    const int e = (int)(k & 31);
+    const int pos = QT == LK_TYPE_Q4_K ? (e & 24) + ((e & 1) ? 4 : 0) + ((e & 7) >> 1)
+                    : QT == LK_TYPE_Q2_K ? (e & 16) + (e & 3) * 4 + ((e & 15) >> 2)
+                                         : e;
+    xs[(k >> 5) * 36 + pos] = *(const float *)(g.b + k * g.b_nb1);
+  }
+  __syncthreads();
+  for (int64_t sbk = tid; sbk < g.K / 32; sbk += ROWS * 64) {
+    const f32x4 *v = (const f32x4 *)(xs + sbk * 36);
+    const f32x4 h0 = (v[0] + v[1]) + (v[2] + v[3]), h1 = (v[4] + v[5]) + (v[6] + v[7]);
+    const float s0 = (h0.x + h0.y) + (h0.z + h0.w), s1 = (h1.x + h1.y) + (h1.z + h1.w);
+    if constexpr (QT == LK_TYPE_Q2_K) {
+      xs[sbk * 36 + 32] = s0;
+      xs[sbk * 36 + 33] = s1;
+    } else {
+      xs[sbk * 36 + 32] = s0 + s1;
     }
-  } else {
-    for (int64_t k = tid; k < g.K; k += ROWS * 64) xs[(k >> 5) * 36 + (k & 31)] = *(const float *)(g.b + k * g.b_nb1);
   }
   __syncthreads();
   const int lane = tid & 63;
@@ -2850,7 +2906,8 @@ __global__ __launch_bounds__(ROWS * 64) void kquant_n1_kernel(KQuantArgs g) {
       const f32x4 *xv = (const f32x4 *)(xs + (min(blk, nb - 1) * 8 + s) * 36);
       float a;
       if constexpr (QT == LK_TYPE_Q4_K) a = kq32_dot_q4k_factored(r[u], s, t, xv, acc);
-      else a = kq32_dot<QT>(r[u], s, t, xv, acc);
+      else if constexpr (QT == LK_TYPE_Q2_K) a = kq32_dot_q2k_factored(r[u], t, xv, acc);
+      else a = kq32_dot_q8k_factored(r[u], xv, acc);
       acc = blk < nb ? a : acc;
     }
   }
