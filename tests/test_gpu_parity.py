@@ -348,6 +348,11 @@ SKINNY = [
     (3000, 2048, 32),
     (50, 384, 20),      # 12 blocks: the second half-slice has 4 blocks (Q4_1; Q4_0 rows are not 16-B)
     (300, 1280, 24),    # 40 blocks: the last slice has no second half
+    # the in-launch split-K reduction at its limits: 64 slices (the largest counter row) over one
+    # row range; 128 slices (past it: the reduce launch instead); many tiles per range at N <= 16
+    (16, 32768, 20),
+    (64, 65536, 8),
+    (5000, 4096, 3),
 ]
 
 
