@@ -1817,10 +1817,13 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
 #define LK_PTRACE(slot_)                                                                                     \
   do {                                                                                                      \
     if (lane == 0 && strace)                                                                                \
-      strace[((size_t)blockIdx.x * NW + wave) * 8 + (slot_)] = __builtin_amdgcn_s_memrealtime();             \
+      strace[((size_t)blockIdx.x * NW + wave) * 16 + (slot_)] = __builtin_amdgcn_s_memrealtime();            \
   } while (0)
+#define LK_PNOW() __builtin_amdgcn_s_memtime()
+  uint64_t c_dma = 0, c_comp = 0, c_issue = 0, c_hand = 0, c_store = 0;  // shader cycles per phase
 #else
 #define LK_PTRACE(slot_) do {} while (0)
+#define LK_PNOW() 0ull
 #endif
   LK_PTRACE(0);
   // XCD-aware task order, as gemm_skinny_kernel
@@ -1957,8 +1960,10 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (myL) {
       // ops younger than this unit's DMA: its successors already issued, and the stores since
+      [[maybe_unused]] const uint64_t q0 = LK_PNOW();
       wait_vmcnt_rt<G::MAXW>(myL * min(D - 1, nunits - 1 - u) + min(u, D) * SH);
       asm volatile("" ::: "memory");
+      [[maybe_unused]] const uint64_t q1 = LK_PNOW();
       if (u == 0) LK_PTRACE(3);
       uint32_t wd[8][G::WPB];
       {
@@ -1978,25 +1983,39 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       if (nbh == 8) skinny_pair_blocks<QT, NT, G::WPB, true, 0>(wd, tl, nbh, lane, xh, xl, acc);
       else skinny_pair_blocks<QT, NT, G::WPB, false, 0>(wd, tl, nbh, lane, xh, xl, acc);
       wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
+      [[maybe_unused]] const uint64_t q2 = LK_PNOW();
       if (u + D < nunits && LK_SKP_SKEL != 3) issue(u + D, slot);
       if (u == 0) LK_PTRACE(7);
+#ifdef LK_SKINNY_TRACE
+      const uint64_t q3 = LK_PNOW();
+      c_dma += q1 - q0; c_comp += q2 - q1; c_issue += q3 - q2;
+#endif
     }
     f32x4 *xb = xch + ((u & 1) * 4 + p) * NT * 64 + lane;
     if (h == 1) {
       if (LK_SKP_SKEL == 4) continue;
+      [[maybe_unused]] const uint64_t h0 = LK_PNOW();
       // the partner has consumed unit u − 2 (this parity's previous contents)
       while (lds_ld(flags + 8 + p) < u - 1) __builtin_amdgcn_s_sleep(1);
+#ifdef LK_SKINNY_TRACE
+      c_hand += LK_PNOW() - h0;
+#endif
 #pragma unroll
       for (int j = 0; j < NT; j++) xb[j * 64] = acc[j];
       lds_st(flags + 2 * p + (u & 1), u + 1);
     } else {
       if (LK_SKP_SKEL != 4) {
+        [[maybe_unused]] const uint64_t h0 = LK_PNOW();
         while (lds_ld(flags + 2 * p + (u & 1)) != u + 1) __builtin_amdgcn_s_sleep(1);
+#ifdef LK_SKINNY_TRACE
+        c_hand += LK_PNOW() - h0;
+#endif
 #pragma unroll
         for (int j = 0; j < NT; j++) acc[j] += xb[j * 64];
       }
       lds_st(flags + 8 + p, u + 1);
       // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
+      [[maybe_unused]] const uint64_t s0 = LK_PNOW();
       const int t = t0 + p + u * 4;
       const int64_t m = (int64_t)t * 16 + (lane & 15);
 #pragma unroll
@@ -2011,13 +2030,23 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
             if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
         }
       }
+#ifdef LK_SKINNY_TRACE
+      c_store += LK_PNOW() - s0;
+#endif
     }
     if (u == 0) LK_PTRACE(4);
   }
   LK_PTRACE(5);
   wait_vmcnt<0>();
   LK_PTRACE(6);
+#ifdef LK_SKINNY_TRACE  // per-phase shader cycles in slots 8..12
+  if (lane == 0 && strace) {
+    uint64_t *q = strace + ((size_t)blockIdx.x * NW + wave) * 16;
+    q[8] = c_dma; q[9] = c_comp; q[10] = c_issue; q[11] = c_hand; q[12] = c_store;
+  }
+#endif
 #undef LK_PTRACE
+#undef LK_PNOW
   if (g.rsync)
     splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
                             g.d_nb0, g.d_nb1, wave, lane);

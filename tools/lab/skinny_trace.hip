@@ -49,7 +49,8 @@ void run(int M, int K, int N) {
   CK(hipMalloc(&part, 4 * (size_t)slices * M * 32));
   hipLaunchKernelGGL(fill, dim3(256), dim3(256), 0, 0, (uint32_t *)b, (size_t)K * N, 3);
   uint64_t *tb;
-  const size_t nst = (size_t)grid * NW * 8;
+  constexpr int SL = PAIR ? 16 : 8;  // stamp slots per wave (the pair kernel adds phase cycles)
+  const size_t nst = (size_t)grid * NW * SL;
   CK(hipMalloc(&tb, nst * 8));
   CK(hipMemset(tb, 0, nst * 8));
   lk::SkinnyArgs g{};
@@ -80,17 +81,28 @@ void run(int M, int K, int N) {
   std::vector<uint64_t> h(nst);
   CK(hipMemcpy(h.data(), tb, nst * 8, hipMemcpyDeviceToHost));
   uint64_t t0 = ~0ull;
-  for (size_t w = 0; w < (size_t)grid * NW; w++) t0 = std::min(t0, h[w * 8]);
+  for (size_t w = 0; w < (size_t)grid * NW; w++) t0 = std::min(t0, h[w * SL]);
   const char *names[8] = {"entry", "x converted", "barrier", "unit0 landed", "unit0 done", "loop done", "drained",
                           "unit0 computed"};
   for (int k : {0, 1, 2, 3, 7, 4, 5, 6}) {
     std::vector<double> v;
     for (size_t w = 0; w < (size_t)grid * NW; w++)
-      if (h[w * 8 + k]) v.push_back((h[w * 8 + k] - t0) / 100.0);  // us
+      if (h[w * SL + k]) v.push_back((h[w * SL + k] - t0) / 100.0);  // us
     std::sort(v.begin(), v.end());
     if (v.empty()) continue;
     printf("  %-14s n=%5zu  min %7.2f  p10 %7.2f  med %7.2f  p90 %7.2f  max %7.2f us\n", names[k], v.size(), v.front(),
            v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+  }
+  if (PAIR) {  // per-phase shader cycles, per wave, by half (h = 0 collects and stores)
+    const char *ph[5] = {"ring wait (vmcnt)", "LDS reads + blocks", "ring refill issue", "hand-off waits", "stores"};
+    for (int hh = 0; hh < 2; hh++)
+      for (int k = 0; k < 5; k++) {
+        std::vector<double> v;
+        for (size_t w = 0; w < (size_t)grid * NW; w++)
+          if ((int)((w % NW) >> 2) == hh && h[w * SL + 1]) v.push_back((double)h[w * SL + 8 + k]);
+        std::sort(v.begin(), v.end());
+        if (!v.empty()) printf("  h=%d %-20s med %9.0f  p90 %9.0f cycles\n", hh, ph[k], v[v.size() / 2], v[v.size() * 9 / 10]);
+      }
   }
 }
 
