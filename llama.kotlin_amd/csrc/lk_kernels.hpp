@@ -281,6 +281,13 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 #ifndef LK_STREAM_D
 #define LK_STREAM_D 3  // weight units in flight per wave (capped by LDS)
 #endif
+// Lab: LK_STREAM_DYN = c > 0 hands a workgroup's rows to its waves at run time,
+// c units' worth per grab of an LDS counter (after a static first share that covers each wave's
+// prologue), instead of a fixed eighth per wave. The waves then finish together, but the layer
+// launch is slower (26.8-31.0 vs 24.6-25.8 us), so the product keeps the fixed split.
+#ifndef LK_STREAM_DYN
+#define LK_STREAM_DYN 0
+#endif
 #ifndef LK_TIGHT_SLOTS
 #define LK_TIGHT_SLOTS 0
 #endif
@@ -319,9 +326,11 @@ template <int QT, int CPL> struct StreamGeom {
   // unit are masked off) instead of L KB, so more units fit in flight
   static constexpr int SLOT = LK_TIGHT_SLOTS ? (UB + 15) / 16 * 16 : L * 1024;
   static constexpr int IMG = 64 * CPL * 256;              // activation image: 256 B per pair
-  static constexpr int DFIT = (kLdsBytes - IMG) / (kStreamWaves * SLOT);
+  static constexpr int AUX = LK_STREAM_DYN ? 512 : 0;     // row queues (8 x 8 words) + the row counter
+  static constexpr int DFIT = (kLdsBytes - IMG - AUX) / (kStreamWaves * SLOT);
   static constexpr int D = DFIT < LK_STREAM_D ? DFIT : LK_STREAM_D;  // ring depth (units)
-  static constexpr int LDS = IMG + kStreamWaves * D * SLOT;
+  static constexpr int QOFF = IMG + kStreamWaves * D * SLOT;  // LK_STREAM_DYN: wave w's queue at QOFF + 32w, counter at QOFF + 256
+  static constexpr int LDS = QOFF + AUX;
   static constexpr int VMCNT = (D - 1) * L;               // DMA ops allowed in flight past the unit in use
   static_assert(D >= 2, "ring must double-buffer");
   static_assert(VMCNT < 64, "vmcnt field is 6 bits");
@@ -473,6 +482,36 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       rb = min((int)blockIdx.x * per, single.M);
       re = min(rb + per, single.M);
     }
+    const int NP = K >> 6;                         // block pairs per row
+    const int nch = (NP + 63) >> 6;                // units per row
+    const int64_t RB = (int64_t)NP * G::PB;        // row bytes
+#if LK_STREAM_DYN
+    // rows are relative to rb. Wave w first takes rows [w·S, w·S + S) (S rows hold the D units of
+    // its prologue, issued before the barrier that publishes the counter), then one row per grab
+    // of the LDS counter (first value 8·S). A wave's rows are decoded in the order it took them:
+    // their indices wait in its 8-entry LDS queue between the DMA issue and the store.
+    const int R = re - rb;
+    // (a range too short for 8 such shares is split evenly, the counter then starts past it)
+    const int SD = (G::D + nch - 1) / nch;
+    const int S = R >= kStreamWaves * SD ? SD : (R + kStreamWaves - 1) / kStreamWaves;
+    const int s0 = __builtin_amdgcn_readfirstlane(min(wave * S, R));
+    int s_end = __builtin_amdgcn_readfirstlane(min(s0 + S, R));  // end of the wave's current run of rows
+    const int CR = LK_STREAM_DYN > nch ? LK_STREAM_DYN / nch : 1;    // rows per grab
+    const int r0 = rb, row_first = s0;
+    const int nunits = (s_end - s0) * nch;         // units the prologue issues for real
+    LK_LDS int *rowq = (LK_LDS int *)((uint8_t *)lds + G::QOFF) + wave * 8;
+    LK_LDS unsigned *rctr = (LK_LDS unsigned *)((uint8_t *)lds + G::QOFF + 256);
+    int qn = 0;                                    // rows taken (pushed on the queue)
+    bool pending = false, exhausted = false;       // the next row must come from the counter / none left
+    auto push = [&](int r) __attribute__((always_inline)) {
+      if (lane == 0) rowq[qn & 7] = r;
+      ++qn;
+    };
+    auto init_ctr = [&]() __attribute__((always_inline)) {
+      if (wave == 0 && lane == 0) *rctr = (unsigned)(kStreamWaves * S);
+    };
+    if (s0 < s_end) push(s0);
+#else
 #if LK_STREAM_BIAS == 500
     const int per_w = (re - rb + kStreamWaves - 1) / kStreamWaves;
     const int r0 = __builtin_amdgcn_readfirstlane(min(rb + wave * per_w, re));
@@ -485,10 +524,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     const int r0 = __builtin_amdgcn_readfirstlane(min(beg, re));
     const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + (wave < 4 ? pa : pb), re) - r0);
 #endif
-    const int NP = K >> 6;                         // block pairs per row
-    const int nch = (NP + 63) >> 6;                // units per row
-    const int64_t RB = (int64_t)NP * G::PB;        // row bytes
-    const int nunits = nrows * nch;
+    const int nunits = nrows * nch, row_first = 0;
+    auto init_ctr = [&]() __attribute__((always_inline)) {};
+#endif
     const LK_GLOBAL uint8_t *A = (const LK_GLOBAL uint8_t *)a_node + (int64_t)r0 * RB;
 
     // 1. prologue, all by LDS-DMA:
@@ -500,7 +538,18 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     //      instruction k, issued by wave k % 8.
     //    LK_PROLOGUE_ORDER 1 issues weight unit 0 first, then the image, then units 1..D-1:
     //    the HBM stream starts at once and the wait for the image covers unit 0 too.
-    int irow = 0, ich = 0, islot = 0, issued = 0;
+    int irow = row_first, ich = 0, islot = 0, issued = 0;
+    auto advance = [&]() __attribute__((always_inline)) {  // past an issued unit
+      if (++ich == nch) {
+        ich = 0;
+#if LK_STREAM_DYN
+        if (irow + 1 < s_end) push(++irow);
+        else pending = true;  // taken from the counter at the next issue (after the barrier)
+#else
+        ++irow;
+#endif
+      }
+    };
     auto dma_unit = [&](const LK_GLOBAL uint8_t *base, int ubytes, int sl) {
       LK_LDS uint8_t *slot = (LK_LDS uint8_t *)(ring + sl * G::SLOT);
 #pragma unroll
@@ -518,8 +567,24 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       }
     };
     auto issue = [&]() {
+#if LK_STREAM_DYN
+      if (pending) {
+        // by asm: the compiler would drain every LDS-DMA in flight (vmcnt(0)) before an LDS
+        // atomic it cannot tell apart from the ring slots
+        unsigned v = 0;
+        if (lane == 0)
+          asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+                       : "=v"(v) : "v"((uint32_t)(uintptr_t)rctr), "v"((unsigned)CR) : "memory");
+        const int r = (int)__builtin_amdgcn_readfirstlane(v);
+        if (r >= R) { exhausted = true; return; }
+        pending = false;
+        irow = r;
+        s_end = min(r + CR, R);
+        push(r);
+      }
+#endif
       dma_unit(A + (int64_t)irow * RB + (int64_t)ich * G::UB, (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB), islot);
-      if (++ich == nch) { ich = 0; ++irow; }
+      advance();
       islot = (islot + 1 == G::D) ? 0 : islot + 1;
       ++issued;
     };
@@ -569,7 +634,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : (int)min((int64_t)G::UB, RB);
         dma_unit(base, ubytes, k);
         if (real) {
-          if (++ich == nch) { ich = 0; ++irow; }
+          advance();
           ++issued;
         }
       }
@@ -584,6 +649,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       //    one 128-B line each); the shard's last arriver arrives on the top word
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      init_ctr();  // published by the barriers below, before any wave takes a row from it
       unsigned *bsync = sync + (bar - 1) * kChainLine * 9;
       if (wave == 0 && lane == 0) {
         const int sh = (int)blockIdx.x % 8;
@@ -616,6 +682,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       __builtin_amdgcn_s_barrier();
     } else if (sync) {  // chain plans, a later segment of a stage (or stage 0): no grid barrier
       if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
+      init_ctr();
       {  // the first round of activation loads ahead of the weight prologue, waited for alone
         f32x4 xv[4];
         x_issue(0, xv);
@@ -633,6 +700,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       __builtin_amdgcn_s_barrier();
     } else {
     if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
+    init_ctr();
     if (LK_PROLOGUE_ORDER == 0 || LK_PROLOGUE_ORDER == 2) dma_x();
     if (LK_PROLOGUE_ORDER == 2) {  // the image first, alone: its latency is not queued behind the weight burst
       wait_vmcnt<0>();
@@ -681,19 +749,28 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     if (si == 0) LK_TRACE(1);
     int slot = 0, u = 0;
     LK_GLOBAL float *out = (LK_GLOBAL float *)dst_node + (int64_t)r0 * dst_stride;
+#if LK_STREAM_DYN
+    // more_units: another unit may be issued; full_ring: D − 1 units were issued past unit u
+#define LK_MORE_UNITS (!exhausted)
+#define LK_FULL_RING (issued >= u + G::D)
+    for (int dq = 0; dq < qn; dq++) {  // qn grows as the issue side takes rows
+#else
+#define LK_MORE_UNITS (issued < nunits)
+#define LK_FULL_RING (u + G::D - 1 < nunits)
     for (int row = 0; row < nrows; row++) {
+#endif
       float acc = 0.f;
 #pragma unroll
       for (int c = 0; c < CPL; c++) {
         if (c < nch) {
-          if (u + G::D - 1 < nunits) wait_vmcnt<G::VMCNT>();
+          if (LK_FULL_RING) wait_vmcnt<G::VMCNT>();
           else wait_vmcnt<0>();
           const uint32_t *rp = (const uint32_t *)(ring + slot * G::SLOT + lane * G::PB);
           uint32_t w[G::PDW];
 #pragma unroll
           for (int k = 0; k < G::PDW; k++) w[k] = rp[k];
 #if LK_EARLY_ISSUE  // lab: refill the slot before the decode instead of after it
-          if (issued < nunits) {
+          if (LK_MORE_UNITS) {
             wait_lgkmcnt0();
             issue();
           }
@@ -705,7 +782,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 #endif
           acc += valid[c] ? v : 0.f;
 #if !LK_EARLY_ISSUE
-          if (issued < nunits) {
+          if (LK_MORE_UNITS) {
             wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
             issue();
           }
@@ -714,7 +791,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
           ++u;
         }
       }
+#if LK_STREAM_DYN
+      if (si == 0 && dq == 0) LK_TRACE(2);
+      const int row = __builtin_amdgcn_readfirstlane(rowq[dq & 7]);
+#else
       if (si == 0 && row == 0) LK_TRACE(2);
+#endif
 #ifdef LK_NO_REDUCE  // lab: the per-row reduction removed (wrong results)
       const float tot = acc;
 #else
@@ -725,6 +807,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         else out[(int64_t)row * dst_stride] = tot;
       }
     }
+#undef LK_MORE_UNITS
+#undef LK_FULL_RING
   }
   if (sync) {
     // chain plans: the workgroup that leaves last (every workgroup has passed every barrier)
