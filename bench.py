@@ -526,7 +526,7 @@ def _graph_time(torch, fn, s, reps):
 def next_rows(torch, G, dev, reps=20):
     """The SURVEY §8f rows beside the hot path, each at batch 1 on BASELINE shapes, one launch per
     matrix over rotating copies (> Infinity Cache), graph-replayed, algorithmic GB/s:
-    K-quant dots (Q2_K / Q4_K / Q8_K x F32, kquant_gemv_kernel; synthetic super-blocks: random
+    K-quant dots (Q2_K / Q4_K / Q8_K x F32; Q4_K on the stream kernel; synthetic super-blocks: random
     code bytes, scale fields set to 0.01) and the device dequantizeTensor / quantizeTensor of a
     Q4_0 11008x4096 matrix (bytes = blocks in + f32 out, or f32 in + blocks out)."""
     T = G.GGMLType
@@ -562,7 +562,7 @@ def next_rows(torch, G, dev, reps=20):
         nbytes = nb + 4 * K * N + 4 * M * N
         out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
                      "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
-                     "kernel": "kquant_n1_kernel" if N == 1 else ("gemm_sk_kernel<Q4_K> (wave-pair MFMA; activation split and split-K reduction in the kernel)" if 16 <= N <= 32 and qn == "Q4_K" else "kquant_nc_kernel"),
+                     "kernel": ("gemv_stream_kernel<Q4_K> (LDS-DMA stream, 16-block units)" if qn == "Q4_K" else "kquant_n1_kernel") if N == 1 else ("gemm_sk_kernel<Q4_K> (wave-pair MFMA; activation split and split-K reduction in the kernel)" if 16 <= N <= 32 and qn == "Q4_K" else "kquant_nc_kernel"),
                      "rotating_weight_copies": copies, "hip_graph": graphed}
         del g
     # format kernels: dequantize / quantize of a Q4_0 11008 x 4096 matrix

@@ -330,6 +330,7 @@ int launch_stream(int32_t qt, int cpl, int grid, const GemvDesc &single, const S
   LK_STREAM(LK_TYPE_Q4_0, 1) LK_STREAM(LK_TYPE_Q4_0, 2) LK_STREAM(LK_TYPE_Q4_0, 3)
   LK_STREAM(LK_TYPE_Q4_1, 1) LK_STREAM(LK_TYPE_Q4_1, 2) LK_STREAM(LK_TYPE_Q4_1, 3)
   LK_STREAM(LK_TYPE_Q8_0, 1) LK_STREAM(LK_TYPE_Q8_0, 2) LK_STREAM(LK_TYPE_Q8_0, 3)
+  LK_STREAM(LK_TYPE_Q4_K, 1) LK_STREAM(LK_TYPE_Q4_K, 2) LK_STREAM(LK_TYPE_Q4_K, 3)
 #undef LK_STREAM
   return fail(LK_ERR_NOT_IMPLEMENTED, "stream gemv: type %d class %d", qt, cpl);
 }
@@ -975,6 +976,16 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
     static const bool no_n1 = getenv("LK_NO_KQ_N1") != nullptr;  // A/B only
     const size_t xlds = (size_t)(c.K / 32) * 36 * sizeof(float);
     const uintptr_t need = a->type == LK_TYPE_Q4_K ? 15 : 3;
+    // Q4_K at batch 1 on the LDS-DMA stream kernel (a unit = 16 blocks = 64 lanes x 64 items,
+    // the same 2304 B as a Q4_0 unit): rows split over one workgroup per CU, x staged once.
+    // LK_KQ_STREAM=0 keeps kquant_n1_kernel (lab A/B).
+    static const bool kq_stream = [] { const char *e = getenv("LK_KQ_STREAM"); return !e || atoi(e) != 0; }();
+    if (kq_stream && !no_n1 && a->type == LK_TYPE_Q4_K && c.N == 1 && c.K / 64 <= 64 * kStreamMaxUnits &&
+        c.M <= (int64_t)INT32_MAX && c.K <= (int64_t)INT32_MAX && ((uintptr_t)g.a & 15) == 0 && ((uintptr_t)g.b & 15) == 0 &&
+        (c.K == 1 || b->nb[1] == 4) && dst->nb[1] % 4 == 0) {
+      const int cls = (int)((c.K / 64 + 63) / 64);
+      return launch_stream(LK_TYPE_Q4_K, cls, stream_grid(c.M), make_desc(a, b, dst, c), nullptr, 0, st);
+    }
     if (!no_n1 && c.N == 1 && ((uintptr_t)g.a & need) == 0 && xlds <= 64 * 1024) {
       const dim3 grid((unsigned)((c.M + 15) / 16)), block(1024);
       switch (a->type) {

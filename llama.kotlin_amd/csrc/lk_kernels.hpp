@@ -317,8 +317,13 @@ struct StreamWork {
 static_assert(sizeof(StreamWork) == 64, "one s_load_dwordx16");
 constexpr int kChainLine = 32;  // chain sync words: one per 128-B line
 
+template <int QT> constexpr int stream_pb() {
+  if constexpr (QT == LK_TYPE_Q4_K) return LK_Q4_K_BLOCK_BYTES / 4;
+  else return 2 * QTraits<QT>::BB;
+}
 template <int QT, int CPL> struct StreamGeom {
-  static constexpr int PB = 2 * QTraits<QT>::BB;         // bytes per block pair
+  // bytes per 64 items (a lane's share of a unit): a block pair, or a quarter Q4_K block
+  static constexpr int PB = stream_pb<QT>();
   static constexpr int PDW = PB / 4;
   static constexpr int UB = 64 * PB;                      // bytes per unit
   static constexpr int L = (UB + 1023) / 1024;            // DMA instructions per unit
@@ -326,10 +331,12 @@ template <int QT, int CPL> struct StreamGeom {
   // unit are masked off) instead of L KB, so more units fit in flight
   static constexpr int SLOT = LK_TIGHT_SLOTS ? (UB + 15) / 16 * 16 : L * 1024;
   static constexpr int IMG = 64 * CPL * 256;              // activation image: 256 B per pair
-  static constexpr int AUX = LK_STREAM_DYN ? 512 : 0;     // row queues (8 x 8 words) + the row counter
+  // LK_STREAM_DYN: row queues (8 x 8 words) + the row counter; Q4_K: the table i/63 (64 floats)
+  static constexpr int AUX = (LK_STREAM_DYN ? 512 : 0) + (QT == LK_TYPE_Q4_K ? 256 : 0);
   static constexpr int DFIT = (kLdsBytes - IMG - AUX) / (kStreamWaves * SLOT);
   static constexpr int D = DFIT < LK_STREAM_D ? DFIT : LK_STREAM_D;  // ring depth (units)
   static constexpr int QOFF = IMG + kStreamWaves * D * SLOT;  // LK_STREAM_DYN: wave w's queue at QOFF + 32w, counter at QOFF + 256
+  static constexpr int TOFF = QOFF + (LK_STREAM_DYN ? 512 : 0);  // Q4_K: the i/63 table
   static constexpr int LDS = QOFF + AUX;
   static constexpr int VMCNT = (D - 1) * L;               // DMA ops allowed in flight past the unit in use
   static_assert(D >= 2, "ring must double-buffer");
@@ -425,6 +432,13 @@ __device__ __forceinline__ float dpp_sum(float v) {
   return v;
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// A lane's 64 items of a Q4_K unit (two 32-item sub-blocks of one block; defined with the
+// K-quant dots below): header h (d, dmin, the 12 scale bytes), the sub-blocks' codes c0, c1.
+__device__ float q4k_stream_dot(const u32x4 &h, const u32x4 &c0, const u32x4 &c1, int lane, const f32x4 *xr, float xs0,
+                                float xs1, const float *q63);
+
 // Optional per-wave timeline (tools/lab/trace.hip defines LK_STREAM_TRACE): s_memrealtime
 // (100 MHz) at kernel entry, activations in VGPRs, first unit decoded, and exit.
 #ifdef LK_STREAM_TRACE
@@ -452,6 +466,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint8_t *ring = (uint8_t *)lds + G::IMG + wave * (G::D * G::SLOT);
+  float *q63 = (float *)((uint8_t *)lds + G::TOFF);  // Q4_K only; published by the prologue's barrier
+  if constexpr (QT == LK_TYPE_Q4_K)
+    if (tid < 64) q63[tid] = __fdiv_rn((float)tid, 63.0f);
   LK_TRACE(0);
   const StreamWork *wk = work ? work + (int64_t)blockIdx.x * spw : nullptr;
   const int nseg = wk ? ((const __attribute__((address_space(4))) int32_t *)wk)[offsetof(StreamWork, count) / 4] : 1;
@@ -767,8 +784,16 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
           else wait_vmcnt<0>();
           const uint32_t *rp = (const uint32_t *)(ring + slot * G::SLOT + lane * G::PB);
           uint32_t w[G::PDW];
+          u32x4 kh, kc0, kc1;  // Q4_K: block lane/4's header and sub-blocks 2(lane%4), +1
+          if constexpr (QT == LK_TYPE_Q4_K) {
+            const uint8_t *bp = ring + slot * G::SLOT + (lane >> 2) * LK_Q4_K_BLOCK_BYTES;
+            kh = *(const u32x4 *)bp;
+            kc0 = *(const u32x4 *)(bp + 4 + LK_K_SCALE_SIZE + 32 * (lane & 3));
+            kc1 = *(const u32x4 *)(bp + 20 + LK_K_SCALE_SIZE + 32 * (lane & 3));
+          } else {
 #pragma unroll
-          for (int k = 0; k < G::PDW; k++) w[k] = rp[k];
+            for (int k = 0; k < G::PDW; k++) w[k] = rp[k];
+          }
 #if LK_EARLY_ISSUE  // lab: refill the slot before the decode instead of after it
           if (LK_MORE_UNITS) {
             wait_lgkmcnt0();
@@ -778,7 +803,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 #ifdef LK_NO_DECODE  // lab: the decode removed (wrong results): the DMA + LDS-read skeleton alone
           const float v = __builtin_bit_cast(float, w[0] ^ w[G::PDW - 1]);
 #else
-          const float v = pair_dot_s<QT>(w, xr[c], xs0[c], xs1[c]);
+          float v;
+          if constexpr (QT == LK_TYPE_Q4_K) v = q4k_stream_dot(kh, kc0, kc1, lane, xr[c], xs0[c], xs1[c], q63);
+          else v = pair_dot_s<QT>(w, xr[c], xs0[c], xs1[c]);
 #endif
           acc += valid[c] ? v : 0.f;
 #if !LK_EARLY_ISSUE
@@ -2919,6 +2946,52 @@ __device__ __forceinline__ float kq32_dot_q4k_factored(const Kq32Raw<LK_TYPE_Q4_
   const float sx = ((const float *)xv)[32];            // Σ x of the sub-block
   const float part = __fdiv_rn(sq, 15.0f) * scale;
   return a + (part + off * sx);
+}
+
+// Q4_K in the stream kernel (gemv_stream_kernel<Q4_K>): the lane's two sub-blocks s = 2(lane%4)
+// and s + 1, each as kq32_dot_q4k_factored computes it (the same scale/min decoding of the
+// Kotlin layout, :274-306; (Σ q·x)/15·scale + off·Σx, correctly rounded quotient, nothing
+// contracted), with the activations and Σx the stream kernel holds in VGPRs and i/63 from LDS.
+__device__ float q4k_stream_dot(const u32x4 &h, const u32x4 &c0, const u32x4 &c1, int lane, const f32x4 *xr, float xs0,
+                                float xs1, const float *q63) {
+#pragma clang fp contract(off)
+  const float d = h2f(h.x & 0xFFFF), dmin = h2f(h.x >> 16);
+  // sub-blocks s = 2j + q (j = lane % 4): scale bytes 4 + s = the 16-bit field at byte 4 + 2j;
+  // the min's high bits from byte 5 + 2s = byte 1 + 2q of header dword j + 1 (none for j = 3,
+  // s >= 6: byte 4 + 2s + 1 would lie past the 12 scale bytes)
+  const int j = lane & 3;
+  const uint32_t scw = (j < 2 ? h.y : h.z) >> (16 * (j & 1));
+  const uint32_t mw = j == 0 ? h.y : j == 1 ? h.z : j == 2 ? h.w : 0u;
+  constexpr float r15 = 1.0f / 15.0f;
+  float a = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint32_t sc = (scw >> (8 * q)) & 0xFF;          // (sext8(sc) >> 6) & 3 == sc >> 6
+    const uint32_t qm = (sc >> 6) | (((mw >> (8 + 16 * q)) & 0x0F) << 2);
+    const float scale = q63[sc & 0x3F] * d;
+    const float off = q63[qm] * d + dmin;
+    const u32x4 c = q ? c1 : c0;
+    const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+    f2v s2 = {0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const uint32_t lo = cw[t] & 0x0F0F0F0Fu, hi = (cw[t] >> 4) & 0x0F0F0F0Fu;
+      const f32x4 xa = xr[8 * q + 2 * t], xb = xr[8 * q + 2 * t + 1];
+      s2 = __builtin_elementwise_fma(fp8x2<false>(lo), f2v{xa.x, xa.y}, s2);
+      s2 = __builtin_elementwise_fma(fp8x2<true>(lo), f2v{xa.z, xa.w}, s2);
+      s2 = __builtin_elementwise_fma(fp8x2<false>(hi), f2v{xb.x, xb.y}, s2);
+      s2 = __builtin_elementwise_fma(fp8x2<true>(hi), f2v{xb.z, xb.w}, s2);
+    }
+    const float sq = (s2.x + s2.y) * 512.f;
+    // sq / 15 correctly rounded without the division sequence: q0 = RN(sq·RN(1/15)) is faithful,
+    // the remainder sq − 15·q0 is exact by FMA, and one corrected step RN(q0 + r·RN(1/15)) is the
+    // correctly rounded quotient (Markstein); one-hot inputs check it bit for bit
+    const float q0 = sq * r15;
+    const float rem = __builtin_fmaf(-q0, 15.0f, sq);
+    const float quo = __builtin_fmaf(rem, r15, q0);
+    a = a + (quo * scale + off * (q ? xs1 : xs0));
+  }
+  return a;
 }
 
 // Q2_K at batch 1, factored the same way per 16-item sub-block (:182-196): (Σ q·x)/3·scale +

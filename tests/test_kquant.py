@@ -191,3 +191,41 @@ def test_kquant_gpu_errors_like_oracle(gpu, qt):
     short = G.GGMLTensor(G.GGMLType(qt), [256, 1], bufferId=ga.addBuffer(BB[qt] - 4))
     with pytest.raises(G.IndexOutOfBoundsException):  # the block runs past the buffer
         G.computeMatMul(ga, ga.context, short, b2, G.GGMLTensor(G.GGMLType.F32, [1, 1], bufferId=idd))
+
+
+# Q4_K at batch 1 runs on the LDS-DMA stream kernel (gemv_stream_kernel<Q4_K>, units of 16
+# blocks) when A and x are 16-byte aligned and K <= 12288: one, two and three units per row,
+# a partial last unit (11008 = 43 blocks), ragged and tiny row counts, fewer rows than waves.
+Q4K_STREAM = [(11008, 4096, 1), (4096, 11008, 1), (300, 8192, 1), (3, 12288, 1), (5, 256, 1), (129, 2816, 1),
+              (2049, 1024, 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", Q4K_STREAM, ids=lambda s: "x".join(map(str, s)))
+def test_q4_k_stream_vs_oracle(gpu, shape):
+    from test_gpu_parity import gpu_matmul
+    M, K, N = shape
+    raw = random_kblocks(Q4_K, M * K // 256, seed=3 * M + K)
+    x = _x(K, N, 17 + M)
+    ref = O.mat_mul_q(Q4_K, raw, M, K, x)
+    got = gpu_matmul(Q4_K, raw, M, K, N, x)
+    ok, msg = parity_ok(got, ref)
+    assert ok, msg
+    again = gpu_matmul(Q4_K, raw, M, K, N, x)
+    assert np.array_equal(got.view(np.uint32), again.view(np.uint32)), "not deterministic"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [8192, 11008])
+def test_q4_k_stream_weights_bit_exact(gpu, K):
+    """One-hot activations through the stream kernel's Q4_K units (2 and 3 units per row, the
+    last one partial at 11008): every output is one Kotlin weight, bit for bit."""
+    from test_gpu_parity import gpu_matmul
+    M = 40
+    raw = random_kblocks(Q4_K, M * K // 256, seed=K + 1)
+    for k in (0, 63, 64, 4095, 4096 + 200, K - 257, K - 1):
+        x = np.zeros((K, 1), np.float32)
+        x[k, 0] = 1.0
+        ref = O.mat_mul_q(Q4_K, raw, M, K, x)
+        got = gpu_matmul(Q4_K, raw, M, K, 1, x)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k

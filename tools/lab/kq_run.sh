@@ -1,0 +1,6 @@
+cd "${GRAFT_REPO_ROOT}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_kquant.py -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/kq_pytest.log 2>&1
+rc=$?; tail -n 4 gpurun_out/kq_pytest.log; [ $rc -eq 0 ] || exit $rc
+tools/lab/kq_stream_ab.sh
