@@ -267,8 +267,14 @@ hipStream_t pick_stream(void *s) { return (hipStream_t)s; }
 
 // Fast grouped GEMV eligibility: batch 1, K % 64 == 0, 4-byte aligned A, 16-byte
 // aligned contiguous x, F32 dst with unit column stride irrelevant (N == 1).
+// Q4_K rides the streaming kernel too (16-block units; K % 256 == 0), in plans and chains as
+// well as single launches; the other K-quants keep their own kernels.
+bool stream_kquant(const lk_tensor *a, const Checked &c) {
+  return c.path == Path::kKQuantF32 && a->type == LK_TYPE_Q4_K && c.K % LK_QK_K == 0;
+}
+
 bool gemv_eligible(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const Checked &c) {
-  if (c.path != Path::kQuantF32 || c.N != 1 || c.K <= 0 || (c.K % 64) != 0) return false;
+  if (!(c.path == Path::kQuantF32 || stream_kquant(a, c)) || c.N != 1 || c.K <= 0 || (c.K % 64) != 0) return false;
   if (c.M > (int64_t)INT32_MAX || c.K > (int64_t)INT32_MAX) return false;
   if (((uintptr_t)a->data + a->data_offset) % 4) return false;
   if (((uintptr_t)b->data + b->data_offset) % 16) return false;
@@ -295,11 +301,14 @@ GemvDesc make_desc(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
 // LDS-DMA streaming kernel eligibility on top of gemv_eligible: at most kStreamMaxUnits
 // units of 64 block pairs per row, rows a whole number of 16-byte DMA lanes, A 16-aligned.
 // Returns the units-per-row class (1..kStreamMaxUnits) or 0.
+// Bytes of A per 64 items as the streaming kernel cuts rows (a block pair; a quarter Q4_K block).
+int stream_pair_bytes(int32_t t) { return is_q(t) ? 2 * block_bytes(t) : t == LK_TYPE_Q4_K ? LK_Q4_K_BLOCK_BYTES / 4 : 0; }
+
 int stream_class(const lk_tensor *a, const Checked &c) {
   const int64_t np = c.K / 64;
   const int64_t nch = (np + 63) / 64;
   if (nch < 1 || nch > kStreamMaxUnits) return 0;
-  if ((np * 2 * block_bytes(a->type)) % 16) return 0;
+  if (!stream_pair_bytes(a->type) || (np * stream_pair_bytes(a->type)) % 16) return 0;
   if (((uintptr_t)a->data + a->data_offset) % 16) return 0;
   return (int)nch;
 }
@@ -980,12 +989,9 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
     // the same 2304 B as a Q4_0 unit): rows split over one workgroup per CU, x staged once.
     // LK_KQ_STREAM=0 keeps kquant_n1_kernel (lab A/B).
     static const bool kq_stream = [] { const char *e = getenv("LK_KQ_STREAM"); return !e || atoi(e) != 0; }();
-    if (kq_stream && !no_n1 && a->type == LK_TYPE_Q4_K && c.N == 1 && c.K / 64 <= 64 * kStreamMaxUnits &&
-        c.M <= (int64_t)INT32_MAX && c.K <= (int64_t)INT32_MAX && ((uintptr_t)g.a & 15) == 0 && ((uintptr_t)g.b & 15) == 0 &&
-        (c.K == 1 || b->nb[1] == 4) && dst->nb[1] % 4 == 0) {
-      const int cls = (int)((c.K / 64 + 63) / 64);
-      return launch_stream(LK_TYPE_Q4_K, cls, stream_grid(c.M), make_desc(a, b, dst, c), nullptr, 0, st);
-    }
+    if (kq_stream && !no_n1 && gemv_eligible(a, b, dst, c))
+      if (const int cls = stream_class(a, c))
+        return launch_stream(LK_TYPE_Q4_K, cls, stream_grid(c.M), make_desc(a, b, dst, c), nullptr, 0, st);
     if (!no_n1 && c.N == 1 && ((uintptr_t)g.a & need) == 0 && xlds <= 64 * 1024) {
       const dim3 grid((unsigned)((c.M + 15) / 16)), block(1024);
       switch (a->type) {
@@ -1500,7 +1506,7 @@ const bool g_straddle = [] {
 }();
 
 void split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<std::vector<StreamWork>> &per) {
-  const int64_t pb = 2 * block_bytes(qt);
+  const int64_t pb = stream_pair_bytes(qt);
   const size_t n = descs.size();
   // Whole nodes per workgroup when there are workgroups enough: node i gets a share of the grid
   // proportional to its bytes (largest remainder, at least one), its rows split evenly over

@@ -229,3 +229,63 @@ def test_q4_k_stream_weights_bit_exact(gpu, K):
         ref = O.mat_mul_q(Q4_K, raw, M, K, x)
         got = gpu_matmul(Q4_K, raw, M, K, 1, x)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+
+
+@pytest.mark.gpu
+def test_q4_k_plan_and_chain_equal_single_launches(gpu):
+    """Q4_K nodes in lk_plan (independent nodes, one grouped launch) and lk_plan_create_chain
+    (dependent stages, one persistent launch): bit-identical to single launches, which match the
+    oracle; the Llama-7B-like stage shapes {q,k,v} -> o -> {gate, up} -> down."""
+    import torch
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="cuda", defaultBufferSize=16)
+    dims, fanout = [4096, 4096, 4096, 11008, 4096], [3, 1, 2, 1]
+    xb = ga.addBuffer(4 * dims[0] + 64)
+    x = G.GGMLTensor(G.GGMLType.F32, [1, dims[0]], bufferId=xb)
+    ga.setTensorBytes(x, random_acts(dims[0], 5).view(np.uint8))
+    nodes, stages, host_w, cur = [], [], [], x
+    for s in range(len(dims) - 1):
+        K, M = dims[s], dims[s + 1]
+        first = None
+        for f in range(fanout[s]):
+            raw = random_kblocks(Q4_K, M * K // 256, seed=100 + 10 * s + f)
+            a = G.GGMLTensor(G.GGMLType.Q4_K, [K, M], bufferId=ga.addBuffer(raw.size))
+            ga.setTensorBytes(a, raw)
+            d = G.GGMLTensor(G.GGMLType.F32, [1, M], bufferId=ga.addBuffer(4 * M + 64))
+            nodes.append((a, cur, d))
+            stages.append(s)
+            host_w.append((raw, M, K))
+            if first is None:
+                first = d
+        cur = first
+    for (a, b, d) in nodes:
+        G.computeMatMul(ga, ga.context, a, b, d)
+    torch.cuda.synchronize()
+    ref = [ga.tensorBytes(d).cpu().numpy().view(np.float32).copy() for (_, _, d) in nodes]
+    xin = ga.tensorBytes(x).cpu().numpy().view(np.float32).copy()
+    for i in range(fanout[0]):  # the first stage against the oracle
+        raw, M, K = host_w[i]
+        ok, msg = parity_ok(ref[i].reshape(-1, 1), O.mat_mul_q(Q4_K, raw, M, K, xin.reshape(K, 1)))
+        assert ok, (i, msg)
+    # stage 0's independent nodes as one grouped launch
+    plan = G.MulMatPlan(ga, nodes[:fanout[0]])
+    assert plan.numLaunches == 1
+    for (_, _, d) in nodes[:fanout[0]]:
+        ga.tensorBytes(d).fill_(0xFF)
+    plan.launch()
+    torch.cuda.synchronize()
+    for i in range(fanout[0]):
+        got = ga.tensorBytes(nodes[i][2]).cpu().numpy().view(np.float32)
+        assert np.array_equal(got.view(np.uint32), ref[i].view(np.uint32)), i
+    # the whole chain in one launch, twice (the barrier counters re-arm)
+    chain = G.MulMatPlan(ga, nodes, stages=stages)
+    assert chain.numLaunches == 1
+    for rep in range(2):
+        for (_, _, d) in nodes:
+            ga.tensorBytes(d).fill_(0xFF)
+        chain.launch()
+        torch.cuda.synchronize()
+        assert not chain.timedOut()
+        for i, (_, _, d) in enumerate(nodes):
+            got = ga.tensorBytes(d).cpu().numpy().view(np.float32)
+            assert np.array_equal(got.view(np.uint32), ref[i].view(np.uint32)), (rep, i, stages[i])
