@@ -584,6 +584,53 @@ def next_rows(torch, G, dev, reps=20):
                      "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
                      "rotating_copies": copies, "hip_graph": graphed}
     del g
+    out.update(q4_k_layers(torch, G, dev, reps))
+    return out
+
+
+def q4_k_layers(torch, G, dev, reps=20, layers=8):
+    """A Llama-7B layer with Q4_K weights at batch 1 on the stream kernel: the 7 matrices as one
+    grouped launch (MulMatPlan, as `value`'s Q4_0 layer launch) and in the dependent decode order
+    (4 launches per layer, as decode_chain), over `layers` distinct layers (> Infinity Cache),
+    graph-replayed. Synthetic super-blocks as above; each matrix reads a fixed activation vector."""
+    T = G.GGMLType
+    g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+    xs = {}
+    for kind, n in X_LEN.items():
+        xs[kind] = G.GGMLTensor(T.F32, [1, n], bufferId=g.addBuffer(4 * n + 256))
+        g.buffers[xs[kind].bufferId][: 4 * n].copy_(torch.randn(n, device=dev).view(torch.uint8))
+    nodes_by_layer, wbytes = [], 0
+    for _ in range(layers):
+        n = {}
+        for (name, M, K) in LAYER_MATS:
+            nblk = M * K // 256
+            wb = g.addBuffer(nblk * 144 + 256)
+            w = g.buffers[wb][: nblk * 144].view(nblk, 144)
+            w.copy_(torch.randint(0, 256, w.shape, dtype=torch.uint8, device=dev))
+            w[:, 0:4].copy_(torch.tensor([0.01, 0.001], dtype=torch.float16).view(torch.uint8).to(dev))
+            d = G.GGMLTensor(T.F32, [1, M], bufferId=g.addBuffer(4 * M + 256))
+            n[name] = (G.GGMLTensor(T.Q4_K, [K, M], bufferId=wb), xs[X_OF[name]], d)
+            wbytes += nblk * 144 + 4 * K + 4 * M
+        nodes_by_layer.append(n)
+    per_layer_bytes = wbytes / layers
+    s = torch.cuda.Stream(device=dev)
+    out = {}
+    for name, groups in (("q4_k_layer_grouped_n1", [tuple(m for (m, _, _) in LAYER_MATS)]), ("q4_k_layer_decode_chain_n1", CHAIN)):
+        plans = [[G.MulMatPlan(g, [n[k] for k in grp]) for grp in groups] for n in nodes_by_layer]
+
+        def run_all():
+            for lp in plans:
+                for p in lp:
+                    p.launch(stream=s)
+
+        per, graphed = _graph_time(torch, run_all, s, reps)
+        per /= layers
+        out[name] = {"avg_layer_us": round(per * 1e6, 3), "launches_per_layer": len(groups),
+                     "achieved_GBps": round(per_layer_bytes / per / 1e9, 1),
+                     "frac_of_8TBps": round(per_layer_bytes / per / 1e9 / HBM_PEAK_GBS, 4),
+                     "tokens_per_s_32_layers": round(1.0 / (32 * per), 1), "bytes_per_layer": int(per_layer_bytes),
+                     "kernel": "gemv_stream_kernel<Q4_K>", "distinct_layers": layers, "hip_graph": graphed}
+    del g
     return out
 
 

@@ -2960,8 +2960,8 @@ __device__ float q4k_stream_dot(const u32x4 &h, const u32x4 &c0, const u32x4 &c1
   // the min's high bits from byte 5 + 2s = byte 1 + 2q of header dword j + 1 (none for j = 3,
   // s >= 6: byte 4 + 2s + 1 would lie past the 12 scale bytes)
   const int j = lane & 3;
-  const uint32_t scw = (j < 2 ? h.y : h.z) >> (16 * (j & 1));
-  const uint32_t mw = j == 0 ? h.y : j == 1 ? h.z : j == 2 ? h.w : 0u;
+  const uint32_t scw = ((j & 2) ? h.z : h.y) >> (16 * (j & 1));
+  const uint32_t mw = (j & 2) ? ((j & 1) ? 0u : h.w) : ((j & 1) ? h.z : h.y);  // selects, not a switch
   constexpr float r15 = 1.0f / 15.0f;
   float a = 0.f;
 #pragma unroll
