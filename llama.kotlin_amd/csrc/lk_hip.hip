@@ -270,7 +270,7 @@ hipStream_t pick_stream(void *s) { return (hipStream_t)s; }
 // Q4_K rides the streaming kernel too (16-block units; K % 256 == 0), in plans and chains as
 // well as single launches; the other K-quants keep their own kernels.
 bool stream_kquant(const lk_tensor *a, const Checked &c) {
-  return c.path == Path::kKQuantF32 && a->type == LK_TYPE_Q4_K && c.K % LK_QK_K == 0;
+  return c.path == Path::kKQuantF32 && (a->type == LK_TYPE_Q4_K || a->type == LK_TYPE_Q2_K) && c.K % LK_QK_K == 0;
 }
 
 bool gemv_eligible(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const Checked &c) {
@@ -302,7 +302,9 @@ GemvDesc make_desc(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
 // units of 64 block pairs per row, rows a whole number of 16-byte DMA lanes, A 16-aligned.
 // Returns the units-per-row class (1..kStreamMaxUnits) or 0.
 // Bytes of A per 64 items as the streaming kernel cuts rows (a block pair; a quarter Q4_K block).
-int stream_pair_bytes(int32_t t) { return is_q(t) ? 2 * block_bytes(t) : t == LK_TYPE_Q4_K ? LK_Q4_K_BLOCK_BYTES / 4 : 0; }
+int stream_pair_bytes(int32_t t) {
+  return is_q(t) ? 2 * block_bytes(t) : t == LK_TYPE_Q4_K ? LK_Q4_K_BLOCK_BYTES / 4 : t == LK_TYPE_Q2_K ? LK_Q2_K_BLOCK_BYTES / 4 : 0;
+}
 
 int stream_class(const lk_tensor *a, const Checked &c) {
   const int64_t np = c.K / 64;
@@ -340,6 +342,7 @@ int launch_stream(int32_t qt, int cpl, int grid, const GemvDesc &single, const S
   LK_STREAM(LK_TYPE_Q4_1, 1) LK_STREAM(LK_TYPE_Q4_1, 2) LK_STREAM(LK_TYPE_Q4_1, 3)
   LK_STREAM(LK_TYPE_Q8_0, 1) LK_STREAM(LK_TYPE_Q8_0, 2) LK_STREAM(LK_TYPE_Q8_0, 3)
   LK_STREAM(LK_TYPE_Q4_K, 1) LK_STREAM(LK_TYPE_Q4_K, 2) LK_STREAM(LK_TYPE_Q4_K, 3)
+  LK_STREAM(LK_TYPE_Q2_K, 1) LK_STREAM(LK_TYPE_Q2_K, 2) LK_STREAM(LK_TYPE_Q2_K, 3)
 #undef LK_STREAM
   return fail(LK_ERR_NOT_IMPLEMENTED, "stream gemv: type %d class %d", qt, cpl);
 }
@@ -989,9 +992,13 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
     // the same 2304 B as a Q4_0 unit): rows split over one workgroup per CU, x staged once.
     // LK_KQ_STREAM=0 keeps kquant_n1_kernel (lab A/B).
     static const bool kq_stream = [] { const char *e = getenv("LK_KQ_STREAM"); return !e || atoi(e) != 0; }();
-    if (kq_stream && !no_n1 && gemv_eligible(a, b, dst, c))
+    // Q2_K between 2K and 6K rows stays on kquant_n1_kernel: its 1344-B units leave the stream
+    // kernel two per wave there, and the one-shot latency wins (4096^2: 5.45 vs 5.86 us; from
+    // 6144 rows on, and under 2K, the stream kernel is ahead: tools/lab/q2k_run.sh)
+    const bool q2k_mid = a->type == LK_TYPE_Q2_K && c.M > 2048 && c.M < 6144;
+    if (kq_stream && !no_n1 && !q2k_mid && gemv_eligible(a, b, dst, c))
       if (const int cls = stream_class(a, c))
-        return launch_stream(LK_TYPE_Q4_K, cls, stream_grid(c.M), make_desc(a, b, dst, c), nullptr, 0, st);
+        return launch_stream(a->type, cls, stream_grid(c.M), make_desc(a, b, dst, c), nullptr, 0, st);
     if (!no_n1 && c.N == 1 && ((uintptr_t)g.a & need) == 0 && xlds <= 64 * 1024) {
       const dim3 grid((unsigned)((c.M + 15) / 16)), block(1024);
       switch (a->type) {

@@ -319,6 +319,7 @@ constexpr int kChainLine = 32;  // chain sync words: one per 128-B line
 
 template <int QT> constexpr int stream_pb() {
   if constexpr (QT == LK_TYPE_Q4_K) return LK_Q4_K_BLOCK_BYTES / 4;
+  else if constexpr (QT == LK_TYPE_Q2_K) return LK_Q2_K_BLOCK_BYTES / 4;
   else return 2 * QTraits<QT>::BB;
 }
 template <int QT, int CPL> struct StreamGeom {
@@ -332,11 +333,12 @@ template <int QT, int CPL> struct StreamGeom {
   static constexpr int SLOT = LK_TIGHT_SLOTS ? (UB + 15) / 16 * 16 : L * 1024;
   static constexpr int IMG = 64 * CPL * 256;              // activation image: 256 B per pair
   // LK_STREAM_DYN: row queues (8 x 8 words) + the row counter; Q4_K: the table i/63 (64 floats)
-  static constexpr int AUX = (LK_STREAM_DYN ? 512 : 0) + (QT == LK_TYPE_Q4_K ? 256 : 0);
+  static constexpr bool KQ = QT == LK_TYPE_Q4_K || QT == LK_TYPE_Q2_K;
+  static constexpr int AUX = (LK_STREAM_DYN ? 512 : 0) + (KQ ? 256 : 0);
   static constexpr int DFIT = (kLdsBytes - IMG - AUX) / (kStreamWaves * SLOT);
   static constexpr int D = DFIT < LK_STREAM_D ? DFIT : LK_STREAM_D;  // ring depth (units)
   static constexpr int QOFF = IMG + kStreamWaves * D * SLOT;  // LK_STREAM_DYN: wave w's queue at QOFF + 32w, counter at QOFF + 256
-  static constexpr int TOFF = QOFF + (LK_STREAM_DYN ? 512 : 0);  // Q4_K: the i/63 table
+  static constexpr int TOFF = QOFF + (LK_STREAM_DYN ? 512 : 0);  // K-quants: the i/63 (Q4_K) or i/15 (Q2_K) table
   static constexpr int LDS = QOFF + AUX;
   static constexpr int VMCNT = (D - 1) * L;               // DMA ops allowed in flight past the unit in use
   static_assert(D >= 2, "ring must double-buffer");
@@ -438,6 +440,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // K-quant dots below): header h (d, dmin, the 12 scale bytes), the sub-blocks' codes c0, c1.
 __device__ float q4k_stream_dot(const u32x4 &h, const u32x4 &c0, const u32x4 &c1, int lane, const f32x4 *xr, float xs0,
                                 float xs1, const float *q63);
+// A lane's 64 items of a Q2_K unit: four 16-item sub-blocks of one block (scale bytes sc, code
+// dwords c, d | dmin in dd), activations per 16 in bit-pair order, Σx per 16 in xq.
+__device__ float q2k_stream_dot(uint32_t sc, const uint32_t *c, uint32_t dd, const f32x4 *xr, const float *xq,
+                                const float *q15);
 
 // Optional per-wave timeline (tools/lab/trace.hip defines LK_STREAM_TRACE): s_memrealtime
 // (100 MHz) at kernel entry, activations in VGPRs, first unit decoded, and exit.
@@ -466,9 +472,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint8_t *ring = (uint8_t *)lds + G::IMG + wave * (G::D * G::SLOT);
-  float *q63 = (float *)((uint8_t *)lds + G::TOFF);  // Q4_K only; published by the prologue's barrier
+  float *q63 = (float *)((uint8_t *)lds + G::TOFF);  // K-quants only; published by the prologue's barrier
   if constexpr (QT == LK_TYPE_Q4_K)
     if (tid < 64) q63[tid] = __fdiv_rn((float)tid, 63.0f);
+  if constexpr (QT == LK_TYPE_Q2_K)
+    if (tid < 16) q63[tid] = __fdiv_rn((float)tid, 15.0f);
   LK_TRACE(0);
   const StreamWork *wk = work ? work + (int64_t)blockIdx.x * spw : nullptr;
   const int nseg = wk ? ((const __attribute__((address_space(4))) int32_t *)wk)[offsetof(StreamWork, count) / 4] : 1;
@@ -735,7 +743,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 
     // 2. activations into VGPRs in decode order, and Σx per block
     f32x4 xr[CPL][16];
-    float xs0[CPL], xs1[CPL];
+    float xs0[CPL], xs1[CPL], xq[CPL][4];
     bool valid[CPL];
 #pragma unroll
     for (int c = 0; c < CPL; c++) {
@@ -745,7 +753,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 #pragma unroll
       for (int jj = 0; jj < 8; jj++) {
         const f32x4 n0 = lds[16 * pc + ((2 * jj) ^ (pc & 15))], n1 = lds[16 * pc + ((2 * jj + 1) ^ (pc & 15))];
-        if constexpr (QT == LK_TYPE_Q8_0) {
+        if constexpr (QT == LK_TYPE_Q8_0 || QT == LK_TYPE_Q2_K) {
           xr[c][2 * jj] = n0;
           xr[c][2 * jj + 1] = n1;
         } else {  // nibble order: (x0,x2,x4,x6), (x1,x3,x5,x7)
@@ -761,6 +769,18 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       }
       xs0[c] = a0;
       xs1[c] = a1;
+      if constexpr (QT == LK_TYPE_Q2_K) {  // per 16 items: bit-pair order (x_j, x_4+j, x_8+j, x_12+j), Σx
+#pragma unroll
+        for (int g4 = 0; g4 < 4; g4++) {
+          const f32x4 A = xr[c][4 * g4], B = xr[c][4 * g4 + 1], C = xr[c][4 * g4 + 2], Dv = xr[c][4 * g4 + 3];
+          xq[c][g4] = ((A.x + A.y) + (A.z + A.w)) + ((B.x + B.y) + (B.z + B.w)) + (((C.x + C.y) + (C.z + C.w)) +
+                                                                                   ((Dv.x + Dv.y) + (Dv.z + Dv.w)));
+          xr[c][4 * g4] = f32x4{A.x, B.x, C.x, Dv.x};
+          xr[c][4 * g4 + 1] = f32x4{A.y, B.y, C.y, Dv.y};
+          xr[c][4 * g4 + 2] = f32x4{A.z, B.z, C.z, Dv.z};
+          xr[c][4 * g4 + 3] = f32x4{A.w, B.w, C.w, Dv.w};
+        }
+      }
     }
 
     if (si == 0) LK_TRACE(1);
@@ -785,7 +805,14 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
           const uint32_t *rp = (const uint32_t *)(ring + slot * G::SLOT + lane * G::PB);
           uint32_t w[G::PDW];
           u32x4 kh, kc0, kc1;  // Q4_K: block lane/4's header and sub-blocks 2(lane%4), +1
-          if constexpr (QT == LK_TYPE_Q4_K) {
+          uint32_t q2s = 0, q2d = 0, q2c[4];  // Q2_K: scale bytes 4(lane%4).., d | dmin, code dwords
+          if constexpr (QT == LK_TYPE_Q2_K) {
+            const uint32_t *bp = (const uint32_t *)(ring + slot * G::SLOT + (lane >> 2) * LK_Q2_K_BLOCK_BYTES);
+            q2s = bp[lane & 3];
+#pragma unroll
+            for (int t = 0; t < 4; t++) q2c[t] = bp[4 + 4 * (lane & 3) + t];
+            q2d = bp[20];
+          } else if constexpr (QT == LK_TYPE_Q4_K) {
             const uint8_t *bp = ring + slot * G::SLOT + (lane >> 2) * LK_Q4_K_BLOCK_BYTES;
             kh = *(const u32x4 *)bp;
             kc0 = *(const u32x4 *)(bp + 4 + LK_K_SCALE_SIZE + 32 * (lane & 3));
@@ -805,6 +832,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 #else
           float v;
           if constexpr (QT == LK_TYPE_Q4_K) v = q4k_stream_dot(kh, kc0, kc1, lane, xr[c], xs0[c], xs1[c], q63);
+          else if constexpr (QT == LK_TYPE_Q2_K) v = q2k_stream_dot(q2s, q2c, q2d, xr[c], xq[c], q63);
           else v = pair_dot_s<QT>(w, xr[c], xs0[c], xs1[c]);
 #endif
           acc += valid[c] ? v : 0.f;
@@ -2990,6 +3018,36 @@ __device__ float q4k_stream_dot(const u32x4 &h, const u32x4 &c0, const u32x4 &c1
     const float rem = __builtin_fmaf(-q0, 15.0f, sq);
     const float quo = __builtin_fmaf(rem, r15, q0);
     a = a + (quo * scale + off * (q ? xs1 : xs0));
+  }
+  return a;
+}
+
+// Q2_K in the stream kernel (gemv_stream_kernel<Q2_K>): the lane's four 16-item sub-blocks
+// 4(lane%4) + t of block lane/4, each as kq32_dot_q2k_factored computes it ((Σ q·x)/3·scale +
+// min·Σx, :182-196), i/15 from LDS, the quotient by 3 FMA-corrected as for Q4_K.
+__device__ float q2k_stream_dot(uint32_t sc, const uint32_t *c, uint32_t dd, const f32x4 *xr, const float *xq,
+                                const float *q15) {
+#pragma clang fp contract(off)
+  const float d = h2f(dd & 0xFFFF), dmin = h2f(dd >> 16);
+  constexpr float r3 = 1.0f / 3.0f;
+  float a = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const uint32_t sm = (sc >> (8 * t)) & 0xFF;  // (sext8(sm) >> 4) & 0x0F == sm >> 4
+    const float scale = q15[sm & 0x0F] * d;
+    const float mn = (float)(sm >> 4) * d + dmin;
+    f2v s2 = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // bit pair j of each byte: items j, 4 + j, 8 + j, 12 + j
+      const uint32_t b = (c[t] >> (2 * j)) & 0x03030303u;
+      const f32x4 xa = xr[4 * t + j];
+      s2 = __builtin_elementwise_fma(fp8x2<false>(b), f2v{xa.x, xa.y}, s2);
+      s2 = __builtin_elementwise_fma(fp8x2<true>(b), f2v{xa.z, xa.w}, s2);
+    }
+    const float sq = (s2.x + s2.y) * 512.f;
+    const float q0 = sq * r3;
+    const float quo = __builtin_fmaf(__builtin_fmaf(-q0, 3.0f, sq), r3, q0);
+    a = a + (quo * scale + mn * xq[t]);
   }
   return a;
 }

@@ -289,3 +289,37 @@ def test_q4_k_plan_and_chain_equal_single_launches(gpu):
         for i, (_, _, d) in enumerate(nodes):
             got = ga.tensorBytes(d).cpu().numpy().view(np.float32)
             assert np.array_equal(got.view(np.uint32), ref[i].view(np.uint32)), (rep, i, stages[i])
+
+
+# Q2_K at batch 1 on the stream kernel too (its rows are whole 16-byte DMA pieces when
+# K % 1024 == 0): 1-3 units per row, ragged rows; 11008 stays on kquant_n1_kernel.
+Q2K_STREAM = [(11008, 4096, 1), (300, 8192, 1), (3, 12288, 1), (5, 1024, 1), (2049, 1024, 1), (64, 11008, 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", Q2K_STREAM, ids=lambda s: "x".join(map(str, s)))
+def test_q2_k_stream_vs_oracle(gpu, shape):
+    from test_gpu_parity import gpu_matmul
+    M, K, N = shape
+    raw = random_kblocks(Q2_K, M * K // 256, seed=5 * M + K)
+    x = _x(K, N, 23 + M)
+    ref = O.mat_mul_q(Q2_K, raw, M, K, x)
+    got = gpu_matmul(Q2_K, raw, M, K, N, x)
+    ok, msg = parity_ok(got, ref)
+    assert ok, msg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [4096, 12288])
+def test_q2_k_stream_weights_bit_exact(gpu, K):
+    """One-hot activations through the stream kernel's Q2_K units: every output is one Kotlin
+    weight, bit for bit (the FMA-corrected quotient by 3 included)."""
+    from test_gpu_parity import gpu_matmul
+    M = 40
+    raw = random_kblocks(Q2_K, M * K // 256, seed=K + 2)
+    for k in (0, 5, 15, 16, 63, 64, 255, 4095, K - 17, K - 1):
+        x = np.zeros((K, 1), np.float32)
+        x[k, 0] = 1.0
+        ref = O.mat_mul_q(Q2_K, raw, M, K, x)
+        got = gpu_matmul(Q2_K, raw, M, K, 1, x)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k

@@ -15,17 +15,19 @@ G.load_library()
 dev = torch.device("cuda", 0)
 T = G.GGMLType
 out = {}
+QN = os.environ.get("KQ_TYPE", "Q4_K")
 for M, K in ((4096, 4096), (6144, 4096), (8192, 4096), (11008, 4096), (4096, 11008), (32000, 4096), (1024, 4096)):
-    nblk, bb = M * K // 256, 144
+    nblk, bb = M * K // 256, {"Q4_K": 144, "Q2_K": 84}[QN]
+    so = 0 if QN == "Q4_K" else 80
     nb = nblk * bb
     copies = max(2, min(32, (300 << 20) // nb))
     g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
     wb, xb, db = g.addBuffer(copies * nb + 256), g.addBuffer(4 * K + 256), g.addBuffer(4 * M * copies + 256)
     w = g.buffers[wb][: copies * nb].view(copies * nblk, bb)
     w.copy_(torch.randint(0, 256, w.shape, dtype=torch.uint8, device=dev))
-    w[:, 0:4].copy_(torch.tensor([0.01, 0.001], dtype=torch.float16).view(torch.uint8).to(dev))
+    w[:, so:so + 4].copy_(torch.tensor([0.01, 0.001], dtype=torch.float16).view(torch.uint8).to(dev))
     g.buffers[xb][: 4 * K].copy_(torch.randn(K, device=dev).view(torch.uint8))
-    nodes = [(G.GGMLTensor(T.Q4_K, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [1, K], bufferId=xb),
+    nodes = [(G.GGMLTensor(getattr(T, QN), [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [1, K], bufferId=xb),
               G.GGMLTensor(T.F32, [1, M], bufferId=db, dataOffset=4 * M * c)) for c in range(copies)]
     s = torch.cuda.Stream(device=dev)
 
@@ -37,4 +39,4 @@ for M, K in ((4096, 4096), (6144, 4096), (8192, 4096), (11008, 4096), (4096, 110
     per /= copies
     out["%dx%d" % (M, K)] = round(per * 1e6, 3)
     del g
-print(json.dumps({"LK_KQ_STREAM": os.environ.get("LK_KQ_STREAM", "1"), "us": out}))
+print(json.dumps({"type": QN, "LK_KQ_STREAM": os.environ.get("LK_KQ_STREAM", "1"), "us": out}))
