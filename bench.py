@@ -156,16 +156,10 @@ def main():
     # lk_sharded_plan) sits on the path between consecutive layers
     comm = None
     if world > 1 and backend == "nccl":
-        try:
-            comm = G.Comm.from_process_group()
-            plans = [[G.ShardedMulMatPlan(comm, ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
-        except Exception as e:  # noqa: BLE001 — reported in the JSON ("parallelism"), torch's RCCL instead
-            print(f"[bench] lk_comm / lk_sharded_plan failed ({e}); gathering through torch.distributed",
-                  file=sys.stderr)
-            comm = None
-    if comm is not None:
-        pass
-    elif world > 1:  # local launch + torch.distributed gather of the same chunks (gloo rehearsal, or fallback)
+        # the C-ABI's RCCL path is the product: if it cannot be set up the run fails (no fallback)
+        comm = G.Comm.from_process_group()
+        plans = [[G.ShardedMulMatPlan(comm, ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
+    elif world > 1:  # LK_BENCH_BACKEND=gloo rehearsal only: local launch + torch.distributed gather
         plans = [[G.MulMatPlan(ga, lp)] for lp in local_by_layer]
     else:
         plans = [[G.MulMatPlan(ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
@@ -177,7 +171,7 @@ def main():
     obuf_u8 = ga.buffers[obuf]
 
     def gloo_gather(layer):
-        # the in-place all-gather of lk_sharded_plan, through torch.distributed (gloo rehearsal / fallback)
+        # the in-place all-gather of lk_sharded_plan, through torch.distributed (gloo rehearsal only)
         for (name, M, _) in LAYER_MATS:
             d = nodes_by_layer[layer][name][2]
             full = obuf_u8[d.dataOffset:d.dataOffset + 4 * M].view(torch.float32)
@@ -287,8 +281,10 @@ def roofline(torch, plans, local_by_layer, stream, world, reps=10):
     """Dominant kernel: the grouped launch of each layer (all 7 matrices, gemv_stream_kernel<Q4_0,3>).
     A HIP graph of the 32 layer launches (distinct weights per layer, so each launch streams HBM)
     is replayed `reps` times between two events on the launch stream; the mean launch duration is
-    that time / launches (inter-launch gaps inside a graph are included, so this is a lower bound
-    on the kernel's own rate). achieved = algorithmic bytes per launch / mean duration."""
+    that time / launches. It includes the gaps between launches inside the graph, and it is measured
+    un-profiled; rocprof's mean kernel duration for the same launch (profiles/rNN, a profiled run,
+    which lowers the clock) is the other figure DESIGN.md reports beside it — the two differ by a few
+    percent either way. achieved = algorithmic bytes per launch / mean duration."""
     def layers():
         for lp in plans:
             lp[0].launch(stream=stream)
@@ -523,6 +519,16 @@ def _graph_time(torch, fn, s, reps):
     return e0.elapsed_time(e1) / 1e3 / reps, gr is not None
 
 
+def _kquant_kernel(qn, M, K, N):
+    """The kernel launch_kquant (csrc/lk_hip.hip) picks for these dense, 256-B aligned operands."""
+    if N == 1:
+        stream = (qn == "Q4_K" or (qn == "Q2_K" and (M <= 2048 or M >= 6144) and (K // 64 * 21) % 16 == 0))
+        return f"gemv_stream_kernel<{qn}> (LDS-DMA stream)" if stream and K <= 12288 else "kquant_n1_kernel"
+    if qn == "Q4_K" and 16 <= N <= 32:
+        return "gemm_sk_kernel<Q4_K> (wave-pair MFMA; activation split and split-K reduction in the kernel)"
+    return "kquant_nc_kernel"
+
+
 def next_rows(torch, G, dev, reps=20):
     """The SURVEY §8f rows beside the hot path, each at batch 1 on BASELINE shapes, one launch per
     matrix over rotating copies (> Infinity Cache), graph-replayed, algorithmic GB/s:
@@ -562,7 +568,7 @@ def next_rows(torch, G, dev, reps=20):
         nbytes = nb + 4 * K * N + 4 * M * N
         out[name] = {"avg_launch_us": round(per * 1e6, 3), "achieved_GBps": round(nbytes / per / 1e9, 1),
                      "frac_of_8TBps": round(nbytes / per / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": nbytes,
-                     "kernel": ("gemv_stream_kernel<Q4_K> (LDS-DMA stream, 16-block units)" if qn == "Q4_K" else "kquant_n1_kernel") if N == 1 else ("gemm_sk_kernel<Q4_K> (wave-pair MFMA; activation split and split-K reduction in the kernel)" if 16 <= N <= 32 and qn == "Q4_K" else "kquant_nc_kernel"),
+                     "kernel": _kquant_kernel(qn, M, K, N),
                      "rotating_weight_copies": copies, "hip_graph": graphed}
         del g
     # format kernels: dequantize / quantize of a Q4_0 11008 x 4096 matrix
@@ -787,7 +793,7 @@ def host_path(torch, G, dev, layers=LAYERS, reps=5):
     for a, b, d in nodes:
         d.op, d.src = G.GGMLOp.MUL_MAT, [a, b]
         dsts.append(d)
-    be = G.GGMLHipBackend(ga)
+    be = G.GGMLHipBackend(ga, wholeGraphs=True)  # the token's whole MUL_MAT graph in one call
     cg = G.GGMLCGraph(dsts, ga)
     if be.graphCompute(cg) != G.GGMLStatus.SUCCESS:
         raise RuntimeError("GGMLHipBackend.graphCompute failed")
@@ -795,7 +801,7 @@ def host_path(torch, G, dev, layers=LAYERS, reps=5):
     for _ in range(reps):
         be.graphCompute(cg)
     per = (time.perf_counter() - t0) / reps * lay
-    mask = G.backend.writeBackMask(dsts)
+    mask = G.backend.writeBackMask(dsts, wholeGraph=True)
     res["backend"] = {"ms_per_token": round(per * 1e3, 3), "tokens_per_s": round(1 / per, 2),
                       "d2h_bytes_per_token": int(sum(4 * d.ne[0] * d.ne[1] for d, w in zip(dsts, mask) if w) * lay),
                       "path": "GGMLHipBackend.graphCompute -> cached lk_graph (ggml_hip/backend.py)"}

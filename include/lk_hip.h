@@ -192,11 +192,22 @@ int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor
 int lk_plan_chain_timed_out(lk_plan *plan);
 void lk_plan_destroy(lk_plan *plan);
 /* Batched MUL_MATs (2 <= N) reduce their K slices inside the launch, workgroups waiting for each
- * other (every workgroup co-resident: at most one per CU). *count = how many of those waits on
- * the current device gave up at their 200 ms bound since the last call (the results of those
- * launches are undefined; never seen with one process per GPU), then resets the count.
- * Synchronizes the device. Diagnostic; no reference counterpart. */
+ * other (every workgroup co-resident: at most one per CU), and chain plans wait at grid barriers.
+ * Every such wait is bounded (200 ms). A wait that gives up raises a per-device flag: the next
+ * synchronous entry point on that device (lk_mul_mat, lk_mul_mat_sharded, lk_graph_compute)
+ * returns LK_ERR_DEVICE instead of LK_OK — those results are undefined (GGMLStatus.FAILED at
+ * backend level, core/GGMLCpuBackend.kt:167-176). Stream-ordered entry points (lk_mul_mat_device,
+ * lk_plan_launch) cannot report it at launch; a caller of those reads it here:
+ * *count = how many waits on the current device gave up since the last call; the count and the
+ * flag are then reset. Synchronizes the device. Diagnostic; no reference counterpart. */
 int lk_sync_timeouts(uint32_t *count);
+/* Test hooks of the same mechanism (current device; synchronize it first):
+ * lk_set_sync_wait_bound — the wait bound in 100 MHz ticks (default 20000000 = 200 ms); 0 makes a
+ *   waiter that does not find its peers already arrived give up at once (tests of the error path);
+ * lk_sync_counters_sum — the sum of every split-K arrival/departure counter word, 0 between
+ *   launches (the counters re-arm inside each launch). */
+int lk_set_sync_wait_bound(uint64_t ticks);
+int lk_sync_counters_sum(uint64_t *sum);
 
 /* ---- multi-GPU: row shards + RCCL all-gather over xGMI -----------------
  * The reference is single-device; this is the north star's partition of the same operator.
@@ -216,6 +227,11 @@ int lk_comm_init_rank(const void *id, int nranks, int rank, lk_comm **out);
 int lk_comm_init_all(int ndev, const int *devices, lk_comm **comms);
 int lk_comm_nranks(const lk_comm *comm);
 int lk_comm_rank(const lk_comm *comm);
+/* The HIP device the communicator's rank runs on. */
+int lk_comm_device(const lk_comm *comm);
+/* How many ncclAllGather calls were enqueued through the communicator (a HIP-graph replay of
+ * captured ones does not count again). */
+uint64_t lk_comm_num_collectives(const lk_comm *comm);
 void lk_comm_destroy(lk_comm *comm);
 int lk_comm_group_start(void);
 int lk_comm_group_end(void);
@@ -232,6 +248,8 @@ int lk_sharded_plan_create(lk_comm *comm, const lk_tensor *a, const lk_tensor *b
 int lk_sharded_plan_launch(lk_sharded_plan *plan, void *stream);
 int lk_sharded_plan_num_gathers(const lk_sharded_plan *plan);
 void lk_sharded_plan_destroy(lk_sharded_plan *plan);
+/* lk_sharded_plan_launch always issues its RCCL group, at one rank too (in-place copies), so the
+ * one-GPU tests run the code a multi-GPU node runs. */
 
 /* ---- graph residency over host buffers ---------------------------------------
  * GGMLComputeOps.computeGraph / computeMulMat (core/GGMLComputeOps.kt:2515-2652) for a
@@ -246,6 +264,23 @@ void lk_sharded_plan_destroy(lk_sharded_plan *plan);
 typedef struct lk_graph lk_graph;
 int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
                     const uint8_t *outputs, uint64_t weight_generation, lk_graph **out);
+/* The same graph row-sharded over the GPUs of a node (the north star's partition behind the
+ * graph API): every quantized weight node whose rows split evenly (M % P == 0, K % 32 == 0, dense
+ * F32 dst) runs rank r's rows [r·M/P, (r+1)·M/P) on rank r's device — only that shard of the
+ * weight is pinned there — into the full dst mirror, and one in-place RCCL all-gather per level
+ * completes every dst on every device, so the next level reads whole activations on each. Other
+ * nodes run whole on every device. Results are the bytes lk_graph_create's graph produces.
+ *   ncomms == 1: comms[0] is this process's rank (one process per GPU; lk_comm_init_rank, or a
+ *                one-rank communicator); the graph runs on its device, HIP-graph replayed.
+ *   ncomms  > 1: comms[r] = rank r of lk_comm_init_all (one thread drives every device); each
+ *                level's launches and all-gathers of all devices form one RCCL group; outputs are
+ *                read back from rank 0's device.
+ * The communicators must outlive the graph. */
+int lk_graph_create_sharded(lk_comm *const *comms, int ncomms, const lk_tensor *a, const lk_tensor *b,
+                            const lk_tensor *dst, int n, const uint8_t *outputs, uint64_t weight_generation,
+                            lk_graph **out);
+/* Nodes of the graph that run row-sharded (0 for lk_graph_create's graphs). */
+int lk_graph_num_sharded(const lk_graph *g);
 /* Upload inputs, run, write outputs back; synchronous. */
 int lk_graph_compute(lk_graph *g);
 int lk_graph_num_levels(const lk_graph *g);

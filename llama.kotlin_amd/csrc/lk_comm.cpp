@@ -40,6 +40,7 @@ int failf(int st, const char *what, ncclResult_t r) {
 struct lk_comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0, device = 0;
+  uint64_t collectives = 0;  // ncclAllGather calls enqueued through this communicator
 };
 
 struct lk_sharded_plan {
@@ -48,6 +49,22 @@ struct lk_sharded_plan {
   struct Gather { void *full; uint64_t chunk; };
   std::vector<Gather> gathers;             // per node: in-place all-gather of chunk bytes per rank
 };
+
+namespace {
+
+// Runs f with the communicator's device current (one host thread may drive several devices:
+// lk_comm_init_all), then restores the caller's device.
+template <typename F>
+int on_device(int dev, F f) {
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) prev = dev;
+  if (prev != dev && hipSetDevice(dev) != hipSuccess) return lk_detail_fail(LK_ERR_DEVICE, "comm: cannot select its device");
+  const int rc = f();
+  if (prev != dev) (void)hipSetDevice(prev);
+  return rc;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -93,6 +110,8 @@ int lk_comm_init_all(int ndev, const int *devices, lk_comm **out) {
 
 int lk_comm_nranks(const lk_comm *c) { return c ? c->nranks : 0; }
 int lk_comm_rank(const lk_comm *c) { return c ? c->rank : -1; }
+int lk_comm_device(const lk_comm *c) { return c ? c->device : -1; }
+uint64_t lk_comm_num_collectives(const lk_comm *c) { return c ? c->collectives : 0; }
 
 void lk_comm_destroy(lk_comm *c) {
   if (!c) return;
@@ -141,30 +160,37 @@ int lk_sharded_plan_create(lk_comm *comm, const lk_tensor *a, const lk_tensor *b
     ld[i].data_offset = d.data_offset + (uint64_t)r * chunk;
     p->gathers.push_back({(uint8_t *)d.data + d.data_offset, chunk});
   }
-  const int rc = lk_plan_create(la.data(), lb.data(), ld.data(), n, &p->local);
+  const int rc = on_device(comm->device, [&] { return lk_plan_create(la.data(), lb.data(), ld.data(), n, &p->local); });
   if (rc) { delete p; return rc; }
   *out = p;
   return LK_OK;
 }
 
+// The local launch, then one RCCL group of in-place all-gathers — at every world size: at one rank
+// the gathers are RCCL's (trivial) in-place copies, so the code path a multi-GPU node runs is the
+// one the one-GPU tests exercise. Inside an outer lk_comm_group_start / end (one thread driving
+// several devices) the gathers join that group.
 int lk_sharded_plan_launch(lk_sharded_plan *p, void *stream) {
   if (!p) return lk_detail_fail(LK_ERR_INVALID_ARG, "null sharded plan");
   hipStream_t st = (hipStream_t)stream;
-  int rc = lk_plan_launch(p->local, stream);
-  if (rc) return rc;
-  if (p->comm->nranks == 1 || p->gathers.empty()) return LK_OK;  // the local rows are the whole dst
-  NCCL_TRY(ncclGroupStart(), "ncclGroupStart");
-  for (auto &g : p->gathers) {
-    uint8_t *full = (uint8_t *)g.full;
-    const ncclResult_t r = ncclAllGather(full + (uint64_t)p->comm->rank * g.chunk, full, g.chunk, ncclChar,
-                                         p->comm->comm, st);
-    if (r != ncclSuccess) {
-      (void)ncclGroupEnd();
-      return failf(LK_ERR_DEVICE, "ncclAllGather", r);
+  return on_device(p->comm->device, [&]() -> int {
+    int rc = lk_plan_launch(p->local, stream);
+    if (rc) return rc;
+    if (p->gathers.empty()) return LK_OK;
+    NCCL_TRY(ncclGroupStart(), "ncclGroupStart");
+    for (auto &g : p->gathers) {
+      uint8_t *full = (uint8_t *)g.full;
+      const ncclResult_t r = ncclAllGather(full + (uint64_t)p->comm->rank * g.chunk, full, g.chunk, ncclChar,
+                                           p->comm->comm, st);
+      if (r != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return failf(LK_ERR_DEVICE, "ncclAllGather", r);
+      }
+      p->comm->collectives++;
     }
-  }
-  NCCL_TRY(ncclGroupEnd(), "ncclGroupEnd");
-  return LK_OK;
+    NCCL_TRY(ncclGroupEnd(), "ncclGroupEnd");
+    return LK_OK;
+  });
 }
 
 int lk_sharded_plan_num_gathers(const lk_sharded_plan *p) { return p ? (int)p->gathers.size() : 0; }

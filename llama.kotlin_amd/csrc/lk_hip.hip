@@ -23,9 +23,7 @@
 #include <vector>
 
 #include "lk_kernels.hpp"
-#include "lk_mfma32.hpp"
 #include "lk_skinny.hpp"
-#include "lk_wide2.hpp"
 #include "../../include/lk_gguf.h"
 
 using namespace lk;
@@ -90,6 +88,7 @@ using MirrorRef = std::shared_ptr<Mirror>;
 
 struct Dev {
   hipStream_t stream = nullptr;
+  unsigned *fail_flag = nullptr;  // page-locked word behind lk_sync_fail_flag (lk_kernels.hpp)
   // weight residency cache (host path): the current mirrors of this device (guarded by S().cache_mu)
   std::vector<MirrorRef> weights;
   uint64_t weight_bytes = 0;
@@ -404,7 +403,7 @@ int fused_rsync(int slices, size_t slab_bytes, unsigned **out) {
   if (unfused || slices <= 1 || slices > kRsyncRows || slices > cu || slab_bytes >= (1ull << 31)) return LK_OK;
   GemmScratch &S = gemm_scratch();
   if (!S.rsync) {
-    const int line = (cu + 7) / 8 * 8 + 1;  // a counter per range + the timeout flag after the grid
+    const int line = (cu + 7) / 8 * 8;  // a line per range: arrivals (word 0), departures (word 1)
     const size_t bytes = (size_t)kRsyncRows * line * kChainLine * sizeof(unsigned);
     HIP_TRY(hipMalloc((void **)&S.rsync, bytes));
     HIP_TRY(hipMemset(S.rsync, 0, bytes));
@@ -609,8 +608,7 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   g.rsync = rsync;
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_skinny_pair_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
-  static const bool skip_reduce = getenv("LK_LAB_SKIP_REDUCE") != nullptr;  // lab (wrong results): the reduce's share
-  if (slices > 1 && !fuse && !skip_reduce) {
+  if (slices > 1 && !fuse) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
                        slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);
@@ -619,59 +617,10 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   return LK_OK;
 }
 
-// gemm_q32_kernel (lk_mfma32.hpp): Q4_0 / Q4_1, 17 <= N <= 32, K % 256 == 0, weight rows and base
-// 16-byte aligned, B dense (nb[0] == 4, nb[1] == 4N, N % 4 == 0) and 16-byte aligned.
-bool q32_eligible(const lk_tensor *a, const lk_tensor *b, const Checked &c) {
-  // lab only (LK_Q32=1): measured slower than gemm_skinny_pair_kernel on C3 (28 vs 22 us per call:
-  // an 8 us prologue and ~86 VALU per 32-row block), so off by default
-  static const int mode = [] { const char *e = getenv("LK_Q32"); return e ? atoi(e) : 0; }();
-  if (!mode || (a->type != LK_TYPE_Q4_0 && a->type != LK_TYPE_Q4_1)) return false;
-  if (c.N < (mode == 2 ? 2 : 17) || c.N > 32 || c.N % 4 || c.K % 256) return false;
-  const uint64_t rb = (uint64_t)(c.K / 32) * block_bytes(a->type);
-  const uintptr_t abase = (uintptr_t)a->data + a->data_offset, bbase = (uintptr_t)b->data + b->data_offset;
-  return abase % 16 == 0 && rb % 16 == 0 && rb * 32 < (1ull << 31) && bbase % 16 == 0 && b->nb[0] == 4 &&
-         b->nb[1] == 4 * (uint64_t)c.N;
-}
-
-template <int QT>
-int launch_q32_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
-  using QG = Q32Geom<QT>;
-  GemmScratch &S = gemm_scratch();
-  Q32Args g{};
-  g.a = (const uint8_t *)a->data + a->data_offset;
-  g.b = (const uint8_t *)b->data + b->data_offset;
-  g.dst = (uint8_t *)dst->data + dst->data_offset;
-  g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
-  g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
-  const int nblk = g.K / 32;
-  const int slices = (nblk + QG::SB - 1) / QG::SB;
-  const int ntile = (g.M + 31) / 32;
-  // one workgroup per CU: ranges x slices <= CUs, so every task runs in the first round
-  int ranges = std::max(1, std::min(ntile, cu_count() / slices));
-  g.tiles_per_range = (ntile + ranges - 1) / ranges;
-  ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
-  g.slices = slices;
-  if (slices > 1) {
-    const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 32 * sizeof(float));
-    if (rc) return rc;
-    g.partial = (float *)S.partial;
-  }
-  g.tasks = ranges * slices;
-  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
-  hipLaunchKernelGGL((gemm_q32_kernel<QT>), dim3(grid), dim3(QG::NW * 64), QG::LDS, st, g);
-  if (slices > 1) {
-    const int64_t threads = (int64_t)g.M * (32 / 4);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
-                       slices, g.M, g.N, 32, g.dst, g.d_nb0, g.d_nb1);
-  }
-  HIP_TRY(hipGetLastError());
-  return LK_OK;
-}
-
-// gemm_sk_kernel (lk_skinny.hpp): Q4_0 / Q4_1, 2 <= N <= 32, after skinny_eligible. The
-// activations are split once into MFMA fragments (xsplit_kernel), then the split-K GEMM, then
-// the ordered slab reduction.
-template <int QT, int NT, bool SOLO>
+// gemm_sk_kernel (lk_skinny.hpp): Q4_K x F32, 16 <= N <= 32. Dense, 16-B aligned activations
+// are split by the kernel itself; others go through xsplit_kernel first. Split-K slabs are
+// reduced inside the launch (fused_rsync) or by splitk_reduce_kernel after it.
+template <int QT, int NT>
 int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   using SG = SkGeom<QT, NT>;
   GemmScratch &S = gemm_scratch();
@@ -696,11 +645,9 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
   const int slices = (int)((nblk + SG::SB - 1) / SG::SB);
   const int ntile = (g.M + 15) / 16;
-  // fused split-K reduction (gemm_sk_kernel; the one-wave lab kernel keeps the reduce launch)
   const int cu = cu_count();
   unsigned *rsync = nullptr;
-  if (!SOLO)
-    if (int rf = fused_rsync(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), &rsync)) return rf;
+  if (int rf = fused_rsync(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), &rsync)) return rf;
   int ranges = std::max(1, std::min(ntile, rsync ? cu / slices : (cu + slices - 1) / slices));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
@@ -712,19 +659,11 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   }
   g.tasks = ranges * slices;
   g.rsync = rsync;
-  // dense, 16-B aligned B (every Llama activation): the GEMM splits its slice itself (no xsplit
-  // launch); LK_SK_XSPLIT=1 forces the separate split (lab A/B)
-  static const bool force_xsplit = getenv("LK_SK_XSPLIT") != nullptr;
   g.b = xa.b;
-  g.fx = !SOLO && !force_xsplit && b->nb[0] == 4 && b->nb[1] == 4 * (uint64_t)c.N && ((uintptr_t)xa.b & 15) == 0;
+  g.fx = b->nb[0] == 4 && b->nb[1] == 4 * (uint64_t)c.N && ((uintptr_t)xa.b & 15) == 0;
   if (!g.fx) hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
-  if constexpr (SOLO) {
-    using SG1 = Sk1Geom<QT, NT>;
-    hipLaunchKernelGGL((gemm_sk1_kernel<QT, NT>), dim3(grid), dim3(SG1::NW * 64), SG1::LDS, st, g);
-  } else {
-    hipLaunchKernelGGL((gemm_sk_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
-  }
+  hipLaunchKernelGGL((gemm_sk_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
   if (slices > 1 && !rsync) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
@@ -735,21 +674,6 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
 }
 
 int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
-  // Lab (LK_SK=1: gemm_sk_kernel, wave pairs; LK_SK=2: gemm_sk1_kernel, one wave per SIMD; both
-  // lk_skinny.hpp): parity-green, measured slower than the kernels below on C3 (27 / 29 vs 23 us
-  // per call), so off by default; DESIGN.md §3 has the timeline.
-  static const int sk = [] { const char *e = getenv("LK_SK"); return e ? atoi(e) : 0; }();
-  if (sk && (a->type == LK_TYPE_Q4_0 || a->type == LK_TYPE_Q4_1)) {
-    const bool one = c.N <= 16;
-#define LK_SKL(S) \
-    if (a->type == LK_TYPE_Q4_0) return one ? launch_sk_t<LK_TYPE_Q4_0, 1, S>(a, b, dst, c, st) : launch_sk_t<LK_TYPE_Q4_0, 2, S>(a, b, dst, c, st); \
-    return one ? launch_sk_t<LK_TYPE_Q4_1, 1, S>(a, b, dst, c, st) : launch_sk_t<LK_TYPE_Q4_1, 2, S>(a, b, dst, c, st);
-    if (sk == 2) { LK_SKL(true) }
-    LK_SKL(false)
-#undef LK_SKL
-  }
-  if (q32_eligible(a, b, c))
-    return a->type == LK_TYPE_Q4_0 ? launch_q32_t<LK_TYPE_Q4_0>(a, b, dst, c, st) : launch_q32_t<LK_TYPE_Q4_1>(a, b, dst, c, st);
   SkinnyArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
   g.b = (const uint8_t *)b->data + b->data_offset;
@@ -819,29 +743,13 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
   const int nsuper = ((g.tiles_m + g.sm - 1) / g.sm) * ((g.tiles_n + g.sn - 1) / g.sn);
   g.tasks = nsuper * g.sm * g.sn * slices;
   const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
-  static const int w2 = [] { const char *e = getenv("LK_WIDE2"); return e ? atoi(e) : 0; }();
   // fused split-K reduction in gemm_wide_kernel when every task is co-resident (one per CU)
   g.rsync = nullptr;
-  if (!w2 && g.tasks <= cu_count())
+  if (g.tasks <= cu_count())
     if (int rf = fused_rsync(slices, (size_t)slices * g.M * npad * sizeof(float), &g.rsync)) return rf;
-  // LK_WIDE2=1 / 2: gemm_wide2_kernel (lk_wide2.hpp, dedicated loader waves, 4 / 8 consumers) on the same tiles; its
-  // Q4 codes are 128 + n, so the activations come in xsplit's q4_order 2 with T = MULT·Σ(hi + lo)
-  XSplitArgs xw = xa;
-  if (w2 && QT != LK_TYPE_Q8_0) {
-    xw.q4_order = 2;
-    xw.mult = Wide2Geom<QT>::MULT;
-  }
-  static const bool skip_xsplit = getenv("LK_LAB_SKIP_XSPLIT") != nullptr;  // lab (wrong results): the split's share
-  if (!skip_xsplit) hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xw);
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
-  if (w2 == 2) {
-    using G8 = Wide2Geom<QT, 8>;
-    hipLaunchKernelGGL((gemm_wide2_kernel<QT, 8>), dim3(grid), dim3(G8::NW * 64), G8::LDS, st, g);
-  } else if (w2) {
-    using G4 = Wide2Geom<QT, 4>;
-    hipLaunchKernelGGL((gemm_wide2_kernel<QT, 4>), dim3(grid), dim3(G4::NW * 64), G4::LDS, st, g);
-  }
-  else hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
+  hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
   if (slices > 1 && !g.rsync) {
     const int64_t threads = (int64_t)g.M * (npad / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
@@ -1015,7 +923,7 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
     static const bool kq_sk = [] { const char *e = getenv("LK_KQ_SK"); return !e || atoi(e) != 0; }();
     if (kq_sk && a->type == LK_TYPE_Q4_K && c.N >= 16 && c.N <= 32 && ((uintptr_t)g.a & 15) == 0 &&
         (uint64_t)(c.K / LK_QK_K) * LK_Q4_K_BLOCK_BYTES * 16 < (1ull << 31))
-      return c.N <= 16 ? launch_sk_t<LK_TYPE_Q4_K, 1, false>(a, b, dst, c, st) : launch_sk_t<LK_TYPE_Q4_K, 2, false>(a, b, dst, c, st);
+      return c.N <= 16 ? launch_sk_t<LK_TYPE_Q4_K, 1>(a, b, dst, c, st) : launch_sk_t<LK_TYPE_Q4_K, 2>(a, b, dst, c, st);
     // batch > 1: NC columns per workgroup staged in LDS (NC = 8 / 4 / 2 as K allows)
     const size_t col_lds = (size_t)(c.K / 32) * 36 * sizeof(float);
     int nc = 0;
@@ -1104,7 +1012,25 @@ int init_dev(int d) {
   HIP_TRY(hipSetDevice(d));
   Dev &v = S().devs[d];
   if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+  if (!v.fail_flag) {  // the word a device-side wait raises when it gives up (lk_note_timeout)
+    unsigned *f = nullptr;
+    HIP_TRY(hipHostMalloc((void **)&f, 64, hipHostMallocCoherent));
+    *(volatile unsigned *)f = 0;
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(lk_sync_fail_flag), &f, sizeof(f)));
+    v.fail_flag = f;
+  }
   return LK_OK;
+}
+
+// After a host synchronisation of device d: LK_ERR_DEVICE (and the flag re-armed) when one of the
+// device-side waits of the launches since the last check gave up — their results are undefined.
+int sync_failures(int d) {
+  Dev &v = S().devs[d];
+  if (!v.fail_flag || !__atomic_load_n(v.fail_flag, __ATOMIC_ACQUIRE)) return LK_OK;
+  __atomic_store_n(v.fail_flag, 0u, __ATOMIC_RELEASE);
+  return fail(LK_ERR_DEVICE,
+              "device %d: a split-K or chain wait gave up at its bound (workgroups not co-resident: another launch "
+              "shares the GPU); the results of that launch are undefined", d);
 }
 
 // The current mirror covering host bytes [lo, hi) of base on this device, or null.
@@ -1320,7 +1246,7 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync((uint8_t *)dst->data + c.d_lo, s.scratch[2], d_bytes, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  return LK_OK;
+  return sync_failures(S().device);
 }
 
 // ---- row-sharded host operator: one process, several GPUs (SURVEY §8b lk_mul_mat_sharded) -----
@@ -1467,6 +1393,8 @@ int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, i
   for (int d = 0; d < ndev; d++)
     if (used[d] && hipStreamSynchronize(S().devs[d].stream) != hipSuccess && rc == LK_OK)
       rc = fail(LK_ERR_DEVICE, "sharded: device %d failed", d);
+  for (int d = 0; d < ndev; d++)
+    if (used[d] && rc == LK_OK) rc = sync_failures(d);
 out:
   (void)hipSetDevice(prev);
   return rc;
@@ -1715,6 +1643,7 @@ int lk_plan_chain_timed_out(lk_plan *plan) {
   if (hipMemcpy(&flag, plan->sync + words - kChainLine, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess) return fail(LK_ERR_DEVICE, "chain: flag");
   if (flag) {
     (void)hipMemset(plan->sync, 0, (size_t)words * sizeof(unsigned));
+    (void)sync_failures(S().device);  // reported here instead
     return 1;
   }
   return 0;
@@ -1730,7 +1659,30 @@ int lk_sync_timeouts(uint32_t *count) {
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(lk_sync_timeout_count), sizeof(v)) != hipSuccess ||
       hipMemcpyToSymbol(HIP_SYMBOL(lk_sync_timeout_count), &zero, sizeof(zero)) != hipSuccess)
     return fail(LK_ERR_DEVICE, "timeout count");
+  (void)sync_failures(S().device);  // reported here instead
   *count = v;
+  return LK_OK;
+}
+
+int lk_set_sync_wait_bound(uint64_t ticks) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(lk_sync_wait_bound), &ticks, sizeof(ticks)));
+  return LK_OK;
+}
+
+int lk_sync_counters_sum(uint64_t *sum) {
+  if (!sum) return fail(LK_ERR_INVALID_ARG, "null sum");
+  int rc = ensure_init();
+  if (rc) return rc;
+  *sum = 0;
+  GemmScratch &G = gemm_scratch();
+  if (!G.rsync) return LK_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<unsigned> w((size_t)kRsyncRows * G.rsync_line * kChainLine);
+  HIP_TRY(hipMemcpy(w.data(), G.rsync, w.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+  for (unsigned x : w) *sum += x;
   return LK_OK;
 }
 
@@ -1864,10 +1816,22 @@ struct lk_graph {
   uint64_t generation = 0;
   int nlev = 0;
   std::vector<Region> regions;
-  std::vector<lk_plan *> levels;
-  std::vector<int> plan_level;  // dependency level each plan of `levels` runs
+  // per non-empty dependency level: one plan of the nodes every device computes whole and, on a
+  // sharded graph, one sharded plan of the row-sharded nodes (their in-place all-gathers after it)
+  struct Level { lk_plan *plan = nullptr; lk_sharded_plan *sp = nullptr; };
+  std::vector<Level> levels;
   // per node: host A descriptor, checks, weight flag, device descriptors, bound weight mirror
   std::vector<lk_tensor> ha, da, db, dd;
+  // row sharding over an RCCL communicator (lk_graph_create_sharded): a node with shard[i] runs
+  // this rank's rows of its weight (device descriptor sa[i], rows [rank·M/P, (rank+1)·M/P)) into
+  // the full dst mirror, which the in-place all-gather then completes on every rank
+  lk_comm *comm = nullptr;
+  int nranks = 1, rank = 0;
+  std::vector<char> shard;
+  std::vector<lk_tensor> sa;
+  // one host thread driving several devices (lk_comm_init_all): a sub-graph per device; this
+  // graph only orchestrates (uploads to every part, levels in RCCL groups, outputs from part 0)
+  std::vector<lk_graph *> parts;
   std::vector<Checked> c;
   std::vector<char> a_weight;
   std::vector<MirrorRef> pins;
@@ -1908,10 +1872,16 @@ std::vector<Span> merge_spans(std::vector<Span> v) {
 // pinned last), else it is pinned from the host bytes with the graph's generation. Called at
 // create and again by lk_graph_compute when one of the bound mirrors went stale (superseded
 // or evicted): plans and the captured HIP graph hold raw device pointers, so both are rebuilt.
-int graph_bind(lk_graph *g, bool at_create) {
-  for (auto *p : g->levels) lk_plan_destroy(p);
+void destroy_levels(lk_graph *g) {
+  for (auto &L : g->levels) {
+    if (L.plan) lk_plan_destroy(L.plan);
+    if (L.sp) lk_sharded_plan_destroy(L.sp);
+  }
   g->levels.clear();
-  g->plan_level.clear();
+}
+
+int graph_bind(lk_graph *g, bool at_create) {
+  destroy_levels(g);
   if (g->exec) (void)hipGraphExecDestroy(g->exec);
   g->exec = nullptr;
   g->computes = 0;  // first compute after a bind runs eager (sizes scratch), then capture
@@ -1920,24 +1890,53 @@ int graph_bind(lk_graph *g, bool at_create) {
   for (int i = 0; i < n; i++) {
     if (!g->a_weight[i] || g->c[i].empty) continue;
     const Checked &c = g->c[i];
+    // the bytes this device holds: the whole weight, or this rank's row shard of it
+    lk_tensor src = g->ha[i];
+    uint64_t lo = c.a_lo, hi = c.a_hi;
+    if (g->shard[i]) {
+      const int64_t rows = c.M / g->nranks;
+      const uint64_t pitch = (uint64_t)(c.K / 32) * block_bytes(src.type);
+      src.ne[1] = rows;
+      src.data_offset += (uint64_t)g->rank * rows * pitch;
+      lo = src.data_offset;
+      hi = lo + (uint64_t)rows * pitch;
+    }
     // at create the graph's generation rules (it supersedes other generations over these
     // bytes); at a rebind whatever a caller pinned since is current
-    MirrorRef m = at_create ? nullptr : find_pinned(S().devs[g->device], g->ha[i].data, c.a_lo, c.a_hi);
-    if (!m && (rc = pin_on(g->device, &g->ha[i], c.a_lo, c.a_hi - c.a_lo, g->generation, &m))) return rc;
+    MirrorRef m = at_create ? nullptr : find_pinned(S().devs[g->device], src.data, lo, hi);
+    if (!m && (rc = pin_on(g->device, &src, lo, hi - lo, g->generation, &m))) return rc;
     g->pins[i] = m;
-    g->da[i].data = (uint8_t *)m->ptr + (c.a_lo - m->lo) - c.a_lo;  // base shifted: base + offset = mirror
-    g->da[i].buf_bytes = c.a_hi;
+    lk_tensor &d = g->shard[i] ? g->sa[i] : g->da[i];
+    d = src;
+    d.data = (uint8_t *)m->ptr + (lo - m->lo) - lo;  // base shifted: base + offset = mirror
+    d.buf_bytes = hi;
   }
   for (int l = 0; l < g->nlev; l++) {
-    std::vector<lk_tensor> la, lb, ld;
-    for (int i = 0; i < n; i++)
-      if (g->node_level[i] == l && !g->c[i].empty) { la.push_back(g->da[i]); lb.push_back(g->db[i]); ld.push_back(g->dd[i]); }
-    if (la.empty()) continue;
-    lk_plan *p = nullptr;
-    if ((rc = lk_plan_create(la.data(), lb.data(), ld.data(), (int)la.size(), &p))) return rc;
-    g->levels.push_back(p);
-    g->plan_level.push_back(l);
+    std::vector<lk_tensor> la, lb, ld, sa, sb, sd;
+    for (int i = 0; i < n; i++) {
+      if (g->node_level[i] != l || g->c[i].empty) continue;
+      if (g->shard[i]) { sa.push_back(g->sa[i]); sb.push_back(g->db[i]); sd.push_back(g->dd[i]); }
+      else { la.push_back(g->da[i]); lb.push_back(g->db[i]); ld.push_back(g->dd[i]); }
+    }
+    if (la.empty() && sa.empty()) continue;
+    lk_graph::Level L;
+    if (!la.empty() && (rc = lk_plan_create(la.data(), lb.data(), ld.data(), (int)la.size(), &L.plan))) return rc;
+    if (!sa.empty() && (rc = lk_sharded_plan_create(g->comm, sa.data(), sb.data(), sd.data(), (int)sa.size(), &L.sp))) {
+      if (L.plan) lk_plan_destroy(L.plan);
+      return rc;
+    }
+    g->levels.push_back(L);
   }
+  return LK_OK;
+}
+
+// Enqueue level `l` of g on its device's stream (the caller made g->device current).
+int launch_level(lk_graph *g, size_t l, hipStream_t st) {
+  const lk_graph::Level &L = g->levels[l];
+  if (L.plan)
+    if (int r = lk_plan_launch(L.plan, st)) return r;
+  if (L.sp)
+    if (int r = lk_sharded_plan_launch(L.sp, st)) return r;
   return LK_OK;
 }
 
@@ -1973,7 +1972,8 @@ extern "C" {
 
 void lk_graph_destroy(lk_graph *g) {
   if (!g) return;
-  for (auto *p : g->levels) lk_plan_destroy(p);
+  for (auto *p : g->parts) lk_graph_destroy(p);
+  destroy_levels(g);
   g->pins.clear();
   for (auto &r : g->regions) (void)(r.direct ? hipHostFree(r.alloc) : hipFree(r.alloc));
   if (g->staging) (void)hipHostFree(g->staging);
@@ -1981,12 +1981,14 @@ void lk_graph_destroy(lk_graph *g) {
   delete g;
 }
 
-int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n, const uint8_t *outputs,
-                    uint64_t weight_generation, lk_graph **out) {
-  if (!out || n < 0 || (n && (!a || !b || !dst))) return fail(LK_ERR_INVALID_ARG, "bad graph arguments");
-  *out = nullptr;
-  int rc = ensure_init();
-  if (rc) return rc;
+}  // extern "C"
+
+namespace {
+
+// Builds a graph on the current device (lk_graph_create), or rank comm's part of a sharded one.
+int graph_build(lk_comm *comm, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n, const uint8_t *outputs,
+                uint64_t weight_generation, lk_graph **out) {
+  int rc = LK_OK;
   std::vector<Checked> c(n);
   std::vector<char> a_weight(n, 0);
   std::vector<Span> dsp(n), asp(n), bsp(n);
@@ -2003,7 +2005,10 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
     a_weight[i] = is_q(a[i].type) && !produced && !c[i].empty;
   }
   auto g = new lk_graph();
-  g->device = S().device;
+  if (hipGetDevice(&g->device) != hipSuccess) g->device = S().device;
+  g->comm = comm;
+  g->nranks = comm ? lk_comm_nranks(comm) : 1;
+  g->rank = comm ? lk_comm_rank(comm) : 0;
   g->node_level.assign(n, 0);
   int nlev = 0;
   for (int j = 0; j < n; j++) {  // level = 1 + deepest earlier node it conflicts with
@@ -2058,7 +2063,8 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
   for (auto &s : merge_spans(act)) {
     // the mirror keeps the host address modulo 256, so operands keep their alignment class
     lk_graph::Region r{s.host, s.lo, s.hi, nullptr, nullptr, false};
-    r.direct = !g_no_direct && hits(down_m, s) && !hits(reads, s) && !hits(up_m, s);
+    // (never on a sharded graph: its all-gathers write the dst mirrors)
+    r.direct = !g_no_direct && !comm && hits(down_m, s) && !hits(reads, s) && !hits(up_m, s);
     const uint64_t skew = (s.host + s.lo) & 255;
     const hipError_t e = r.direct ? hipHostMalloc(&r.alloc, s.hi - s.lo + skew, hipHostMallocDefault)
                                   : hipMalloc(&r.alloc, s.hi - s.lo + skew);
@@ -2098,7 +2104,11 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
   g->c = c;
   g->a_weight = a_weight;
   g->pins.assign(n, nullptr);
-  g->da.resize(n); g->db.resize(n); g->dd.resize(n);
+  g->da.resize(n); g->db.resize(n); g->dd.resize(n); g->sa.resize(n);
+  g->shard.assign(n, 0);
+  for (int i = 0; i < n && comm; i++)  // row-shardable: a quantized weight, whole blocks per row, M % P, dense F32 dst
+    g->shard[i] = a_weight[i] && c[i].K % 32 == 0 && c[i].M % g->nranks == 0 && dst[i].type == LK_TYPE_F32 &&
+                  dst[i].nb[0] == 4 && dst[i].nb[1] == 4 * (uint64_t)c[i].N;
   for (int i = 0; i < n; i++) {
     g->da[i] = a[i]; g->db[i] = b[i]; g->dd[i] = dst[i];
     if (c[i].empty) continue;
@@ -2116,8 +2126,9 @@ int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst
   return LK_OK;
 }
 
-int lk_graph_compute(lk_graph *g) {
-  if (!g) return fail(LK_ERR_INVALID_ARG, "null graph");
+// One compute of a single-device graph: staged uploads, every level, staged write-backs on the
+// device's library stream; from the second compute on replayed as one HIP graph.
+int graph_compute_one(lk_graph *g) {
   int rc = lk_init(g->device);
   if (rc) return rc;
   if (graph_stale(g)) {  // a bound weight mirror was superseded or evicted since the last bind
@@ -2125,14 +2136,10 @@ int lk_graph_compute(lk_graph *g) {
     g->rebinds++;
   }
   hipStream_t st = cur().stream;
-  // device part: staged uploads, every level, staged write-backs — replayed as one HIP graph
-  // from the second compute on (the first one sizes any scratch the kernels grow)
   auto enqueue = [&]() -> int {
     for (auto &x : g->h2d) HIP_TRY(hipMemcpyAsync(x.dev, g->staging + x.stage, x.bytes, hipMemcpyHostToDevice, st));
-    for (auto *p : g->levels) {
-      int r = lk_plan_launch(p, st);
-      if (r) return r;
-    }
+    for (size_t l = 0; l < g->levels.size(); l++)
+      if (int r = launch_level(g, l, st)) return r;
     for (auto &x : g->d2h)
       if (!x.direct) HIP_TRY(hipMemcpyAsync(g->staging + x.stage, x.dev, x.bytes, hipMemcpyDeviceToHost, st));
     return LK_OK;
@@ -2154,23 +2161,149 @@ int lk_graph_compute(lk_graph *g) {
   if (g->exec) HIP_TRY(hipGraphLaunch(g->exec, st));
   else if ((rc = enqueue())) return rc;
   HIP_TRY(hipStreamSynchronize(st));
+  if ((rc = sync_failures(g->device))) return rc;  // nothing is written back from a failed launch
   for (auto &x : g->d2h) std::memcpy(x.host, x.direct ? x.dev : g->staging + x.stage, x.bytes);
   g->computes++;
   return LK_OK;
 }
 
-int lk_graph_num_levels(const lk_graph *g) { return g ? (int)g->levels.size() : 0; }
+// One compute of a graph whose parts run on several devices of this thread (eager: uploads to
+// every part, each level of every part inside one RCCL group so the parts' all-gathers meet,
+// outputs read back from part 0, which like every part holds every gathered result).
+int graph_compute_parts(lk_graph *top) {
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  int rc = LK_OK;
+  for (auto *g : top->parts) {
+    if ((rc = init_dev(g->device))) goto out;
+    if (graph_stale(g)) {
+      if ((rc = graph_bind(g, false))) goto out;
+      g->rebinds++;
+    }
+    hipStream_t st = S().devs[g->device].stream;
+    for (auto &x : g->h2d) {
+      std::memcpy(g->staging + x.stage, x.host, x.bytes);
+      if (hipMemcpyAsync(x.dev, g->staging + x.stage, x.bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
+        rc = fail(LK_ERR_DEVICE, "graph: upload to device %d", g->device);
+        goto out;
+      }
+    }
+  }
+  for (size_t l = 0; l < top->parts[0]->levels.size(); l++) {
+    if ((rc = lk_comm_group_start())) goto out;
+    for (auto *g : top->parts) {
+      if ((rc = init_dev(g->device)) || (rc = launch_level(g, l, S().devs[g->device].stream))) break;
+    }
+    const int re = lk_comm_group_end();
+    if (rc || (rc = re)) goto out;
+  }
+  {
+    lk_graph *g0 = top->parts[0];
+    if ((rc = init_dev(g0->device))) goto out;
+    for (auto &x : g0->d2h)
+      if (hipMemcpyAsync(g0->staging + x.stage, x.dev, x.bytes, hipMemcpyDeviceToHost, S().devs[g0->device].stream) != hipSuccess) {
+        rc = fail(LK_ERR_DEVICE, "graph: read back from device %d", g0->device);
+        goto out;
+      }
+  }
+  for (auto *g : top->parts)
+    if (hipSetDevice(g->device) != hipSuccess || hipStreamSynchronize(S().devs[g->device].stream) != hipSuccess) {
+      rc = fail(LK_ERR_DEVICE, "graph: device %d failed", g->device);
+      goto out;
+    }
+  for (auto *g : top->parts)
+    if ((rc = sync_failures(g->device))) goto out;
+  for (auto &x : top->parts[0]->d2h) std::memcpy(x.host, top->parts[0]->staging + x.stage, x.bytes);
+  for (auto *g : top->parts) g->computes++;
+out:
+  (void)hipSetDevice(prev);
+  return rc;
+}
 
-int lk_graph_num_rebinds(const lk_graph *g) { return g ? g->rebinds : 0; }
+}  // namespace
 
+extern "C" {
+
+int lk_graph_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n, const uint8_t *outputs,
+                    uint64_t weight_generation, lk_graph **out) {
+  if (!out || n < 0 || (n && (!a || !b || !dst))) return fail(LK_ERR_INVALID_ARG, "bad graph arguments");
+  *out = nullptr;
+  int rc = ensure_init();
+  if (rc) return rc;
+  return graph_build(nullptr, a, b, dst, n, outputs, weight_generation, out);
+}
+
+int lk_graph_create_sharded(lk_comm *const *comms, int ncomms, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
+                            int n, const uint8_t *outputs, uint64_t weight_generation, lk_graph **out) {
+  if (!out || !comms || ncomms < 1 || n < 0 || (n && (!a || !b || !dst)))
+    return fail(LK_ERR_INVALID_ARG, "bad sharded graph arguments");
+  *out = nullptr;
+  for (int r = 0; r < ncomms; r++)
+    if (!comms[r] || (ncomms > 1 && (lk_comm_nranks(comms[r]) != ncomms || lk_comm_rank(comms[r]) != r)))
+      return fail(LK_ERR_INVALID_ARG, "sharded graph: comms[r] must be rank r of one %d-rank communicator", ncomms);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  int rc = LK_OK;
+  std::vector<lk_graph *> parts;
+  for (int r = 0; r < ncomms && rc == LK_OK; r++) {
+    lk_graph *p = nullptr;
+    if ((rc = init_dev(lk_comm_device(comms[r]))) == LK_OK &&
+        (rc = graph_build(comms[r], a, b, dst, n, outputs, weight_generation, &p)) == LK_OK)
+      parts.push_back(p);
+  }
+  (void)hipSetDevice(prev);
+  if (rc) {
+    for (auto *p : parts) lk_graph_destroy(p);
+    return rc;
+  }
+  if (ncomms == 1) {
+    *out = parts[0];
+    return LK_OK;
+  }
+  auto top = new lk_graph();
+  top->device = parts[0]->device;
+  top->parts = parts;
+  *out = top;
+  return LK_OK;
+}
+
+int lk_graph_compute(lk_graph *g) {
+  if (!g) return fail(LK_ERR_INVALID_ARG, "null graph");
+  return g->parts.empty() ? graph_compute_one(g) : graph_compute_parts(g);
+}
+
+int lk_graph_num_levels(const lk_graph *g) {
+  if (g && !g->parts.empty()) g = g->parts[0];
+  return g ? (int)g->levels.size() : 0;
+}
+
+int lk_graph_num_rebinds(const lk_graph *g) {
+  if (g && !g->parts.empty()) g = g->parts[0];
+  return g ? g->rebinds : 0;
+}
+
+// Kernel launches of one compute on one device (a sharded plan's local launch counts; its
+// all-gathers do not).
 int lk_graph_num_launches(const lk_graph *g) {
+  if (g && !g->parts.empty()) g = g->parts[0];
   int t = 0;
-  if (g) for (auto *p : g->levels) t += lk_plan_num_launches(p);
+  if (g)
+    for (auto &L : g->levels) t += (L.plan ? lk_plan_num_launches(L.plan) : 0) + (L.sp ? 1 : 0);
+  return t;
+}
+
+int lk_graph_num_sharded(const lk_graph *g) {
+  if (g && !g->parts.empty()) g = g->parts[0];
+  int t = 0;
+  if (g)
+    for (char x : g->shard) t += x != 0;
   return t;
 }
 
 uint64_t lk_graph_transfer_bytes(const lk_graph *g, int to_device) {
-  return g ? (to_device ? g->h2d_bytes : g->d2h_bytes) : 0;
+  if (!g) return 0;
+  if (!g->parts.empty()) return to_device ? g->parts.size() * g->parts[0]->h2d_bytes : g->parts[0]->d2h_bytes;
+  return to_device ? g->h2d_bytes : g->d2h_bytes;
 }
 
 }  // extern "C"

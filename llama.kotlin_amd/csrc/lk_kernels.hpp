@@ -317,6 +317,23 @@ struct StreamWork {
 static_assert(sizeof(StreamWork) == 64, "one s_load_dwordx16");
 constexpr int kChainLine = 32;  // chain sync words: one per 128-B line
 
+// Device-side waits (the fused split-K reductions, the chain plans' grid barriers) are bounded:
+// a wait that gives up counts itself in lk_sync_timeout_count (read and reset by lk_sync_timeouts)
+// and raises the host-visible word *lk_sync_fail_flag (page-locked host memory the library
+// installs per device), which every synchronous entry point checks after its sync and turns into
+// LK_ERR_DEVICE: a launch whose wait gave up never reports success. The bound is
+// lk_sync_wait_bound s_memrealtime ticks (100 MHz; 200 ms), changed only by lk_lab_set_sync_bound.
+__device__ unsigned lk_sync_timeout_count;
+__device__ unsigned *lk_sync_fail_flag;
+__device__ uint64_t lk_sync_wait_bound = 20000000ull;
+
+__device__ __forceinline__ void lk_note_timeout() {
+  __hip_atomic_fetch_add(&lk_sync_timeout_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned *f = lk_sync_fail_flag;
+  if (f) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+
 template <int QT> constexpr int stream_pb() {
   if constexpr (QT == LK_TYPE_Q4_K) return LK_Q4_K_BLOCK_BYTES / 4;
   else if constexpr (QT == LK_TYPE_Q2_K) return LK_Q2_K_BLOCK_BYTES / 4;
@@ -688,14 +705,15 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       //    co-resident sets the timeout flag and runs on instead of hanging)
 #ifndef LK_CHAIN_NOWAIT  // lab skeleton (wrong results): the stages run on without waiting
       if (wave == 0 && lane == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), bound = lk_sync_wait_bound;
         const unsigned nsh = gridDim.x < 8 ? gridDim.x : 8;
         while (__hip_atomic_load(bsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nsh) {
-          __builtin_amdgcn_s_sleep(2);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 200 ms at 100 MHz
+          if (__builtin_amdgcn_s_memrealtime() - t0 >= bound) {  // not co-resident: flag it, run on
             __hip_atomic_store(sync + (nbar * 9 + 1) * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lk_note_timeout();
             break;
           }
+          __builtin_amdgcn_s_sleep(2);
         }
       }
 #endif
@@ -1550,17 +1568,16 @@ __device__ __forceinline__ void skinny_blocks(const uint32_t (&w)[SB][WPB], cons
   }
 }
 
-// Waits that gave up at their bound (fused split-K reductions), read and reset by lk_sync_timeouts.
-__device__ unsigned lk_sync_timeout_count;
-
 // Fused split-K reduction (the skinny kernels, gemm_sk_kernel, gemm_wide_kernel): called by every wave of a
 // task once its partial slab rows [m0, m1) of slice `slice` are stored write-through (sc1) and
-// drained. One lane arrives on the row range's counter and waits for the range's other slices (the
-// host launches every task co-resident: at most one workgroup per CU), then the workgroup adds its
-// 1/slices share of the range's rows, slabs in slice order — the order of splitk_reduce_kernel, so
-// the result is bit-identical to it. rsync: the counter row of this `slices` value (each call adds
-// exactly `slices` per range, so every counter is a multiple of slices between calls); a wait
-// past 200 ms counts itself in lk_sync_timeout_count and runs on instead of hanging.
+// drained. One lane arrives on the row range's counter and waits until all `slices` tasks of the
+// range have arrived (the host launches every task co-resident: at most one workgroup per CU),
+// then the workgroup adds its 1/slices share of the range's rows, slabs in slice order — the
+// order of splitk_reduce_kernel, so the result is bit-identical to it.
+// Counters re-arm inside the launch: word 0 of the range's line counts arrivals, word 1
+// departures (a task departs once its wait is over); the last task to depart stores 0 to both,
+// when every task of the range is past its wait. So every launch starts from zeros (no counter
+// ever wraps), whatever the number of calls. One launch at a time per device uses a counter row.
 // Slab rows are N16 floats apart; the range covers columns [n_lo, n_lo + n_cnt) (n_cnt % 4 == 0).
 template <int NW>
 __device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amdgpu_buffer_rsrc_t prs, int range, int slice,
@@ -1569,15 +1586,18 @@ __device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amd
   __builtin_amdgcn_s_barrier();
   if (wave == 0 && lane == 0) {
     unsigned *c = rsync + range * kChainLine;
-    const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = (old / (unsigned)slices + 1u) * (unsigned)slices;
-    const uint64_t ts = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - ts > 20000000ull) {  // 200 ms at 100 MHz: count it, run on
-        __hip_atomic_fetch_add(&lk_sync_timeout_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t ts = __builtin_amdgcn_s_memrealtime(), bound = lk_sync_wait_bound;
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)slices) {
+      if (__builtin_amdgcn_s_memrealtime() - ts >= bound) {  // not co-resident: flag it, run on
+        lk_note_timeout();
         break;
       }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (__hip_atomic_fetch_add(c + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)slices - 1) {
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   asm volatile("" ::: "memory");  // the slab loads stay after the poll

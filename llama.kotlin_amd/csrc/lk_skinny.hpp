@@ -568,195 +568,6 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
                                g.d_nb0, g.d_nb1, wave, lane);
 }
 
-// ---- one wave per SIMD: 16 blocks per wave, no hand-off ----------------------------------------
-//
-// gemm_sk1_kernel: 4 waves (one per SIMD, up to 512 registers each); wave p streams 16-row tiles
-// t0 + p + 4i of its workgroup's row range over the whole 16-block K slice: a unit is 16 rows x
-// 16 blocks (288 / 320 B per row, one pad cell per row so the 16 rows' dwords fall in distinct
-// banks), landed by the wave's own LDS-DMA ring. With the VALU per block at 8 + 1 + NT·2 the
-// lone wave issues its MFMAs and VALU back to back; nothing waits on a partner.
-template <int QT, int NT> struct Sk1Geom {
-  static_assert(QT != LK_TYPE_Q4_K, "Q4_K runs on the wave-pair kernel (a wave's 8 blocks = one Q4_K block)");
-  static constexpr int NW = 4;
-  static constexpr int BB = SkBB<QT>::v;
-  static constexpr int SB = 16;                          // blocks per slice (= per wave)
-  static constexpr int RP = SB * BB;                     // row bytes of a unit (288 / 320)
-  static constexpr int PPR = RP / 16;                    // 16-B cells per row
-  static constexpr int PITCH = RP + 16;                  // LDS row pitch: one pad cell
-  static constexpr int L = (16 * (PPR + 1) + 63) / 64;   // DMA instructions per unit
-  static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : 3;
-  static constexpr int SLOT = L * 1024;
-  static constexpr int XI = SB * NT * kXSplits;
-  static constexpr int XF = XI * 1024;
-  static constexpr int TB = SB * 16 * NT * 4;
-  static constexpr int TI = TB / 1024;
-  static constexpr int DFIT = (kLdsBytes - XF - TB) / (NW * SLOT);
-  static constexpr int D = DFIT > 4 ? 4 : DFIT;
-  static constexpr int LDS = XF + TB + NW * D * SLOT;
-  static constexpr int MAXW = L * (D - 1) + D * NT;
-  static_assert(RP % 16 == 0, "row pieces");
-  static_assert(TB % 1024 == 0, "T DMA");
-  static_assert(D >= 2, "ring must double-buffer");
-  static_assert(LDS <= kLdsBytes, "LDS");
-  static_assert(MAXW < 64, "vmcnt");
-};
-
-template <int QT, int NT>
-__global__ __launch_bounds__(256, 1) void gemm_sk1_kernel(SkArgs g) {
-  using G = Sk1Geom<QT, NT>;
-  constexpr int BB = G::BB, D = G::D, L = G::L, SB = G::SB;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  lu8 *const sbase = (lu8 *)smem;
-  lu8 *xlds = sbase;
-  LK_LDS float *tlds = (LK_LDS float *)(sbase + G::XF);
-  lu8 *ring = sbase + G::XF + G::TB + wave * D * G::SLOT;
-  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
-  if (task >= g.tasks) return;
-  LK_SKT(0, __builtin_amdgcn_s_memrealtime());
-  [[maybe_unused]] uint64_t c_wait = 0, c_comp = 0, c_hand = 0;
-  const int slice = task % g.slices, range = task / g.slices;
-  const int nblk = g.K / 32;
-  const int kb0 = slice * SB, nb = min(SB, nblk - kb0);
-  const int64_t RB = (int64_t)nblk * BB;
-  const int ntile = (g.M + 15) / 16;
-  const int t0 = range * g.tiles_per_range, t1 = min(t0 + g.tiles_per_range, ntile);
-  const int nunits = t1 - t0 - wave > 0 ? (t1 - t0 - wave + 3) / 4 : 0;
-  const int ppr = nb * BB / 16;
-
-  const uint8_t *abase = g.a + (int64_t)kb0 * BB;
-  uint32_t rofs[L];
-  int rrow[L];
-#pragma unroll
-  for (int j = 0; j < L; j++) {
-    const int q = j * 64 + lane, r = q / (G::PPR + 1), c = q % (G::PPR + 1);
-    rrow[j] = min(r, 15);
-    rofs[j] = (uint32_t)((c < ppr && r < 16) ? c * 16 : 0);
-  }
-  auto issue = [&](int u, int sl) __attribute__((always_inline)) {
-    const int t = t0 + wave + u * 4;
-    const uint8_t *tb = abase + (int64_t)t * 16 * RB;
-    const int rmax = g.M - 1 - t * 16;
-#pragma unroll
-    for (int j = 0; j < L; j++) {
-      const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
-      dma16l<LK_SKINNY_NT>(tb, vofs, ring + sl * G::SLOT + j * 1024);
-    }
-  };
-  if (nunits > 0) issue(0, 0);
-  for (int i = wave; i < G::XI; i += G::NW) {
-    const int j = i / (2 * SB), b = (i % (2 * SB)) / 2, sp = i % 2;
-    const int kb = b < nb ? kb0 + b : kb0;
-    dma16l<false>(g.frag, (uint32_t)((((int64_t)j * nblk + kb) * kXSplits + sp) * 1024 + lane * 16), xlds + i * 1024);
-  }
-  {
-    const int n16 = 16 * NT;
-    const int64_t tot = (int64_t)nblk * n16;
-    if (wave < G::TI) {
-      int64_t f = (int64_t)kb0 * n16 + 256 * wave + 4 * lane;
-      if (f + 4 > tot) f = 0;
-      dma16l<false>(g.xsum, (uint32_t)(f * 4), (lu8 *)tlds + wave * 1024);
-    }
-  }
-  for (int u = 1; u < min(D, nunits); u++) issue(u, u);
-  wait_vmcnt_rt<G::MAXW>(L * max(0, min(D - 1, nunits - 1)));
-  __builtin_amdgcn_s_barrier();
-  u32x4 xh[SB][NT], xl[SB][NT];
-#pragma unroll
-  for (int b = 0; b < SB; b++)
-#pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const LK_LDS u32x4 *xf = (const LK_LDS u32x4 *)(xlds + ((j * SB + b) * kXSplits) * 1024) + lane;
-      xh[b][j] = xf[0];
-      xl[b][j] = xf[64];
-      if (b >= nb) {
-        xh[b][j] = u32x4{0u, 0u, 0u, 0u};
-        xl[b][j] = u32x4{0u, 0u, 0u, 0u};
-      }
-    }
-  float sf[4][NT];
-#pragma unroll
-  for (int c = 0; c < 4; c++)
-#pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const int bl = 4 * c + (lane >> 4);
-      sf[c][j] = bl < nb ? tlds[bl * 16 * NT + 16 * j + (lane & 15)] : 0.f;
-    }
-  LK_SKT(1, __builtin_amdgcn_s_memrealtime());
-
-  const int N16 = 16 * NT;
-  for (int u = 0; u < nunits; u++) {
-    const int slot = u % D;
-    f32x4 acc[NT];
-#pragma unroll
-    for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    [[maybe_unused]] const uint64_t c0 = LK_SKT_NOW();
-    // ops younger than this unit's DMA: its successors already issued, and the stores since
-    wait_vmcnt_rt<G::MAXW>(L * min(D - 1, nunits - 1 - u) + NT * min(u, D));
-    asm volatile("" ::: "memory");
-#ifdef LK_SK_TRACE
-    const uint64_t c1 = LK_SKT_NOW();
-    c_wait += c1 - c0;
-    if (u == 0) LK_SKT(2, __builtin_amdgcn_s_memrealtime());
-#endif
-    uint32_t wd[SB][G::WPB];
-    uint32_t eb[4];
-    {
-      const lu8 *bm = ring + slot * G::SLOT + (lane & 15) * G::PITCH;
-      const lu8 *bg = bm + 4 * (lane >> 4);
-      sk_read_all<QT, G::WPB, 0, SB>(bm, bg, wd);
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const lu8 *hp = bm + (4 * c + (lane >> 4)) * BB;
-        if constexpr (QT == LK_TYPE_Q4_1) eb[c] = lds32(hp);
-        else eb[c] = *(const LK_LDS uint16_t *)hp;
-      }
-      asm volatile("" ::: "memory");
-    }
-    f32x4 pp[NT];
-    if (nb == SB) {
-      sk_blocks<QT, NT, G::WPB, false, 0, SB>(wd, xh, xl, nb, pp, 0.f, acc, SkHdr{});
-      sk_interleave<SB * 2 * NT>();
-    } else {
-      sk_blocks<QT, NT, G::WPB, true, 0, SB>(wd, xh, xl, nb, pp, 0.f, acc, SkHdr{});
-    }
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      float e;
-      if constexpr (QT == LK_TYPE_Q4_1) e = fmaf(-128.f, h2f(eb[c]), h2f(eb[c] >> 16));
-      else e = -136.f * h2f(eb[c]);
-      if (4 * c + (lane >> 4) >= nb) e = 0.f;
-#pragma unroll
-      for (int j = 0; j < NT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(sf[c][j], e, acc[j], 0, 0, 0);
-    }
-    wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
-    if (u + D < nunits) issue(u + D, slot);
-#ifdef LK_SK_TRACE
-    c_comp += LK_SKT_NOW() - c1;
-    if (u == 0) LK_SKT(3, __builtin_amdgcn_s_memrealtime());
-#endif
-    const int t = t0 + wave + u * 4;
-    const int64_t m = (int64_t)t * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const int n0 = 16 * j + 4 * (lane >> 4);
-      if (g.slices > 1) {
-        if (m < g.M) *(f32x4 *)(g.partial + (((int64_t)slice * g.M + m) * N16 + n0)) = acc[j];
-      } else if (m < g.M) {
-        const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-          if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
-      }
-    }
-  }
-  LK_SKT(4, __builtin_amdgcn_s_memrealtime());
-  LK_SKT(5, c_wait);
-  LK_SKT(6, c_comp);
-  LK_SKT(7, c_hand);
-  wait_vmcnt<0>();
-}
 #undef LK_SKT
 #undef LK_SKT_NOW
 

@@ -75,12 +75,14 @@ EXPORTED_SYMBOLS = (
     "lk_init", "lk_device_count", "lk_last_error", "lk_shutdown", "lk_version",
     "lk_mul_mat_validate", "lk_mul_mat", "lk_mul_mat_device", "lk_mul_mat_sharded", "lk_weights_pin_sharded",
     "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy", "lk_plan_create_chain",
-    "lk_plan_chain_timed_out", "lk_sync_timeouts",
-    "lk_graph_create", "lk_graph_compute", "lk_graph_num_levels", "lk_graph_num_launches",
+    "lk_plan_chain_timed_out", "lk_sync_timeouts", "lk_set_sync_wait_bound", "lk_sync_counters_sum",
+    "lk_graph_create", "lk_graph_create_sharded", "lk_graph_num_sharded", "lk_graph_compute",
+    "lk_graph_num_levels", "lk_graph_num_launches",
     "lk_graph_transfer_bytes", "lk_graph_destroy", "lk_graph_num_rebinds",
     "lk_weights_pin", "lk_weights_evict", "lk_weights_evict_buffer", "lk_weights_evict_all",
     "lk_weights_cached_bytes", "lk_weights_cached_count",
     "lk_comm_unique_id", "lk_comm_init_rank", "lk_comm_init_all", "lk_comm_nranks", "lk_comm_rank",
+    "lk_comm_device", "lk_comm_num_collectives",
     "lk_comm_destroy", "lk_comm_group_start", "lk_comm_group_end",
     "lk_sharded_plan_create", "lk_sharded_plan_launch", "lk_sharded_plan_num_gathers", "lk_sharded_plan_destroy",
     "lk_dequantize_device", "lk_quantize_device", "lk_dot_direct", "lk_dot_direct_device",
@@ -126,10 +128,15 @@ def load():
     L.lk_plan_create_chain.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.POINTER(vp)]
     L.lk_plan_chain_timed_out.argtypes = [vp]
     L.lk_sync_timeouts.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+    L.lk_set_sync_wait_bound.argtypes = [ctypes.c_uint64]
+    L.lk_sync_counters_sum.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     L.lk_plan_num_launches.argtypes = [vp]
     L.lk_plan_destroy.argtypes = [vp]
     L.lk_plan_destroy.restype = None
     L.lk_graph_create.argtypes = [P, P, P, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(vp)]
+    L.lk_graph_create_sharded.argtypes = [ctypes.POINTER(vp), ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_uint64, ctypes.POINTER(vp)]
+    L.lk_graph_num_sharded.argtypes = [vp]
     L.lk_graph_compute.argtypes = [vp]
     L.lk_graph_num_levels.argtypes = [vp]
     L.lk_graph_num_launches.argtypes = [vp]
@@ -149,6 +156,9 @@ def load():
     L.lk_comm_init_all.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp)]
     L.lk_comm_nranks.argtypes = [vp]
     L.lk_comm_rank.argtypes = [vp]
+    L.lk_comm_device.argtypes = [vp]
+    L.lk_comm_num_collectives.argtypes = [vp]
+    L.lk_comm_num_collectives.restype = ctypes.c_uint64
     L.lk_comm_destroy.argtypes = [vp]
     L.lk_comm_destroy.restype = None
     L.lk_sharded_plan_create.argtypes = [vp, P, P, P, ctypes.c_int, ctypes.POINTER(vp)]

@@ -110,11 +110,17 @@ def _graph_key(ga, nodes, extra) -> tuple:
     return tuple(key)
 
 
-def writeBackMask(nodes) -> list:
-    """Which MUL_MAT results must reach the host ByteArrays: a node flagged as a graph output
-    (GGMLTensor.isOutput, core/GGMLTypes.kt:268) or one no other node of the graph consumes
-    (the caller reads it next: the CPU ops between MUL_MATs in a model graph). Results only
-    consumed by later offloaded nodes stay in HBM."""
+def writeBackMask(nodes, wholeGraph: bool = False) -> list:
+    """Which MUL_MAT results must reach the host ByteArrays.
+
+    By default every one: the graph handed to graphCompute may be one split of a larger graph
+    (GGMLScheduler.executeGraphSplit, core/GGMLScheduler.kt:245-258, passes split subgraphs and
+    sets no output flags), so a node of a later split — a CPU op — may read any result.
+    wholeGraph=True (the caller passes whole graphs): only a node flagged as a graph output
+    (GGMLTensor.isOutput, core/GGMLTypes.kt:268) or one no other node of the graph consumes goes
+    back; results only consumed by later offloaded nodes of the same graph stay in HBM."""
+    if not wholeGraph:
+        return [True] * len(nodes)
     consumed = {id(s) for n in nodes for s in n.src[:2] if s is not None}
     return [n.isOutput() or id(n) not in consumed for n in nodes]
 
@@ -135,12 +141,21 @@ class GGMLHipBackend:
     GUID = "HIP-GFX950-LLAMAKOTLIN"
     MAX_CACHED_GRAPHS = 32
 
-    def __init__(self, graphAllocator=None, device="cuda"):
+    def __init__(self, graphAllocator=None, device="cuda", wholeGraphs: bool = False, shardDevices=None):
+        """wholeGraphs: graphCompute receives whole graphs (see writeBackMask), so results consumed
+        only inside the graph need not be written back. shardDevices: HIP devices to row-shard
+        every host-allocator graph over (lk_graph_create_sharded with one RCCL communicator per
+        device from lk_comm_init_all; a list of one device runs the same path at world size 1)."""
         _lib.load()  # fail loudly when the HIP library is absent
         self._bufferType = GGMLHipBufferType(device)
         self.graphAllocator = graphAllocator
         self.weightGeneration = 0
+        self.wholeGraphs = wholeGraphs
         self._plans: "OrderedDict[tuple, object]" = OrderedDict()
+        self.comms = None
+        if shardDevices:
+            from .sharded import Comm
+            self.comms = Comm.init_all(list(shardDevices))
 
     def getGuid(self) -> str:
         return self.GUID
@@ -152,6 +167,13 @@ class GGMLHipBackend:
         for p in self._plans.values():
             p.close()
         self._plans.clear()
+
+    def close(self):
+        """free() plus the communicators (after every graph that uses them)."""
+        self.free()
+        for c in self.comms or []:
+            c.close()
+        self.comms = None
 
     def bumpWeightGeneration(self) -> int:
         """The host bytes of weights changed: every cached graph re-binds (or is rebuilt) against
@@ -212,9 +234,10 @@ class GGMLHipBackend:
         any operator exception -> FAILED).
 
         Host (ByteArray) allocators: the whole node set is one ResidentGraph (lk_graph), cached
-        by the full tensor descriptors and the weight generation — weights pinned, results that
-        only later nodes consume kept in HBM (writeBackMask), levels of independent nodes grouped
-        into one launch each, the device part replayed as a HIP graph.
+        by the full tensor descriptors and the weight generation — weights pinned, results
+        written back per writeBackMask, levels of independent nodes grouped into one launch
+        each, the device part replayed as a HIP graph; with shardDevices, the graph is
+        row-sharded over those GPUs with an RCCL all-gather per level (lk_graph_create_sharded).
         Device allocators: mutually independent nodes run as one plan, otherwise in order."""
         ga = graph.allocator or self.graphAllocator
         try:
@@ -225,10 +248,10 @@ class GGMLHipBackend:
             if not nodes:
                 return GGMLStatus.SUCCESS
             if _is_host(ga, nodes[0]):
-                mask = writeBackMask(nodes)
+                mask = writeBackMask(nodes, self.wholeGraphs)
                 key = ("host", self.weightGeneration, id(ga), _graph_key(ga, nodes, mask))
                 g = self._cached(key, lambda: ResidentGraph(ga, [(n.src[0], n.src[1], n) for n in nodes], outputs=mask,
-                                                            weightGeneration=self.weightGeneration))
+                                                            weightGeneration=self.weightGeneration, comms=self.comms))
                 g.compute()
                 return GGMLStatus.SUCCESS
             ids = {id(n) for n in nodes}

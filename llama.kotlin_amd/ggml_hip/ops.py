@@ -180,9 +180,14 @@ class ResidentGraph:
 
     ``nodes``: [(a, b, dst)] in graph order; a node reading bytes an earlier node writes runs
     after it. ``outputs``: per-node flags for which dst bytes are written back (None: all).
-    Quantized A operands no node writes are pinned once (``weightGeneration``)."""
+    Quantized A operands no node writes are pinned once (``weightGeneration``).
 
-    def __init__(self, ga: GGMLGraphAllocator, nodes, outputs=None, weightGeneration: int = 0):
+    ``comms``: row-shard the graph over RCCL communicators (lk_graph_create_sharded): a list
+    holding this process's ``sharded.Comm`` (one process per GPU), or every rank's Comm of one
+    ``sharded.Comm.init_all`` (one process driving several GPUs). Weight nodes then run their
+    rank's rows on each device and an in-place all-gather per level completes every result."""
+
+    def __init__(self, ga: GGMLGraphAllocator, nodes, outputs=None, weightGeneration: int = 0, comms=None):
         L = _lib.load()
         n = len(nodes)
         A = (_lib.LkTensor * max(n, 1))()
@@ -194,8 +199,12 @@ class ResidentGraph:
         if outputs is not None:
             outs = (ctypes.c_uint8 * max(n, 1))(*[1 if o else 0 for o in outputs])
         self._handle = ctypes.c_void_p()
-        _lib.check(L.lk_graph_create(A, B, D, n, outs, weightGeneration, ctypes.byref(self._handle)))
-        self._keep = (ga, A, B, D, outs)
+        if comms:
+            H = (ctypes.c_void_p * len(comms))(*[c._handle for c in comms])
+            _lib.check(L.lk_graph_create_sharded(H, len(comms), A, B, D, n, outs, weightGeneration, ctypes.byref(self._handle)))
+        else:
+            _lib.check(L.lk_graph_create(A, B, D, n, outs, weightGeneration, ctypes.byref(self._handle)))
+        self._keep = (ga, A, B, D, outs, comms)
 
     def compute(self):
         _lib.check(_lib.load().lk_graph_compute(self._handle))
@@ -207,6 +216,10 @@ class ResidentGraph:
     @property
     def numLaunches(self) -> int:
         return _lib.load().lk_graph_num_launches(self._handle)
+
+    @property
+    def numSharded(self) -> int:
+        return _lib.load().lk_graph_num_sharded(self._handle)
 
     @property
     def numRebinds(self) -> int:
@@ -346,9 +359,22 @@ def syncTimeouts() -> int:
     return int(n.value)
 
 
+def setSyncWaitBound(ticks: int):
+    """Bound of every device-side wait in 100 MHz ticks (lk_set_sync_wait_bound; default 20000000 =
+    200 ms). Test hook of the failure path: 0 makes the batched kernels' split-K waits give up."""
+    _lib.check(_lib.load().lk_set_sync_wait_bound(int(ticks)))
+
+
+def syncCountersSum() -> int:
+    """Sum of every split-K arrival/departure counter word on the current device (0 between launches)."""
+    v = ctypes.c_uint64(0)
+    _lib.check(_lib.load().lk_sync_counters_sum(ctypes.byref(v)))
+    return int(v.value)
+
+
 def weightsEvictAll():
     _lib.load().lk_weights_evict_all()
 
 
-__all__ = ["syncTimeouts", "computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+__all__ = ["syncTimeouts", "setSyncWaitBound", "syncCountersSum", "computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
            "weightsEvictAll", "weightsEvict", "weightsEvictBuffer", "weightsCachedBytes", "weightsCachedCount", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]

@@ -148,6 +148,28 @@ class Comm:
         return buf.raw
 
     @classmethod
+    def init_all(cls, devices) -> list:
+        """One process driving several GPUs: rank r on devices[r] (lk_comm_init_all)."""
+        import ctypes
+        from . import _lib
+        n = len(devices)
+        devs = (ctypes.c_int * n)(*devices)
+        hs = (ctypes.c_void_p * n)()
+        _lib.check(_lib.load().lk_comm_init_all(n, devs, hs))
+        return [cls(ctypes.c_void_p(hs[r]), n, r) for r in range(n)]
+
+    @property
+    def device(self) -> int:
+        from . import _lib
+        return _lib.load().lk_comm_device(self._handle)
+
+    @property
+    def numCollectives(self) -> int:
+        """ncclAllGather calls enqueued through this communicator so far."""
+        from . import _lib
+        return int(_lib.load().lk_comm_num_collectives(self._handle))
+
+    @classmethod
     def single(cls) -> "Comm":
         """A one-rank communicator (the N = 1 case of the sharded path)."""
         return cls.from_unique_id(cls.unique_id(), 1, 0)

@@ -126,17 +126,32 @@ fun computeDotProductQ80Q80Hip(graphAllocator: GGMLGraphAllocator, a: GGMLTensor
  * (computeGraph, K/core/GGMLComputeOps.kt:2515-2523) and cuts it into runs of consecutive
  * offloadable MUL_MAT nodes. Each run is one lk_graph (include/lk_hip.h), created once and cached
  * by the run's full tensor descriptors and the weight generation: weights stay mirrored in HBM,
- * independent nodes of a dependency level share one launch, the device part is replayed as a
- * HIP graph, and only results that leave the run reach the ByteArrays (those flagged isOutput(),
- * K/core/GGMLTypes.kt:268, read by a node outside the run, or read by no node at all). Nodes the
- * backend does not offload run one at a time on GGMLCpuBackend between the runs.
+ * independent nodes of a dependency level share one launch, and the device part is replayed as a
+ * HIP graph. Every result reaches the ByteArrays by default: the graph may be one split of a larger
+ * one (GGMLScheduler.executeGraphSplit, K/core/GGMLScheduler.kt:245-258, flags no outputs), whose
+ * later splits may read any of them. With wholeGraphs = true (the caller passes whole graphs) only
+ * results that leave the run go back (flagged isOutput(), K/core/GGMLTypes.kt:268, read by a node
+ * outside the run, or read by no node at all). Nodes the backend does not offload run one at a time
+ * on GGMLCpuBackend between the runs.
+ *
+ * shards > 1: the GPUs 0 until shards of the node share every run — one RCCL communicator per GPU
+ * (lk_comm_init_all), each run one lk_graph_create_sharded graph: rank r computes rows
+ * [r·M/P, (r+1)·M/P) of every weight with only that shard pinned on its GPU, and an in-place
+ * all-gather over xGMI per dependency level hands every GPU the whole result (SURVEY §8e).
  *
  * Residency contract: the host ByteArrays stay authoritative. Call bumpWeightGeneration()
  * whenever GGMLGraphAllocator re-places or rewrites tensor bytes (allocateGraph,
  * K/core/GGMLAlloc.kt:404-480) and evictBuffer(old) when reserve replaces a buffer (:392, :638).
  */
-class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) : GGMLBackend {
+class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1,
+                     private val wholeGraphs: Boolean = false) : GGMLBackend {
     private val cpu = GGMLCpuBackend()
+
+    /** shards > 1: rank r's communicator on GPU r (lk_comm_init_all), shared by every sharded run. */
+    private val comms: CPointer<CPointerVar<lk_comm>>? =
+        if (shards > 1) nativeHeap.allocArray<CPointerVar<lk_comm>>(shards).also { arr ->
+            checkStatus(lk_comm_init_all(shards, null, arr))
+        } else null
 
     /** The generation cached weight mirrors are current for (lk_weights_pin semantics). */
     var weightGeneration: ULong = 0u
@@ -168,6 +183,10 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) :
     override fun getName(): String = "HIP"
     override fun free() {
         dropRuns()
+        comms?.let { arr ->
+            for (r in 0 until shards) lk_comm_destroy(arr[r])
+            nativeHeap.free(arr)
+        }
         lk_shutdown()
     }
     override fun getDefaultBufferType(): GGMLBackendBufferType = cpu.getDefaultBufferType()  // host ByteArrays stay authoritative
@@ -221,15 +240,7 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) :
                 }
                 var j = i
                 while (j < nodes.size && supportsOp(nodes[j])) j++
-                if (shards > 1) {
-                    // rows of every MUL_MAT over the node's GPUs: node by node (lk_mul_mat_sharded)
-                    for (k in i until j) {
-                        val n = nodes[k]
-                        computeMatMulHip(ga, ga.context, n.src[0]!!, n.src[1]!!, n, weightGeneration, shards)
-                    }
-                } else {
-                    computeRun(ga, nodes, i, j)
-                }
+                computeRun(ga, nodes, i, j)  // one lk_graph (row-sharded over the GPUs when shards > 1)
                 i = j
             }
             GGMLStatus.SUCCESS
@@ -247,7 +258,7 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) :
         for (n in all) for (s in n.src) if (s != null) readBy.getOrPut(s) { mutableListOf() }.add(n)
         val writeBack = run.map { n ->
             val readers = readBy[n].orEmpty()
-            n.isOutput() || readers.isEmpty() || readers.any { it !in inRun }
+            !wholeGraphs || n.isOutput() || readers.isEmpty() || readers.any { it !in inRun }
         }
         val bufs = ArrayList<ByteArray?>()
         fun buf(t: GGMLTensor): ByteArray? = ga.buffers.getOrNull(t.bufferId)
@@ -290,7 +301,8 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1) :
                 outs[k] = if (writeBack[k]) 1u else 0u
             }
             val h = alloc<CPointerVar<lk_graph>>()
-            val st = lk_graph_create(la, lb, ld, n, outs, weightGeneration, h.ptr)
+            val st = if (comms != null) lk_graph_create_sharded(comms, shards, la, lb, ld, n, outs, weightGeneration, h.ptr)
+                     else lk_graph_create(la, lb, ld, n, outs, weightGeneration, h.ptr)
             if (st != LK_OK.toInt()) {
                 pins.forEach { it.unpin() }
                 checkStatus(st)

@@ -429,23 +429,21 @@ def test_c1_f32_512_cubed(gpu, oracle):
     assert ok, msg
 
 
-# 32x32x16 MFMA GEMM for Q4_0 / Q4_1 at 17 <= N <= 32 (N % 4 == 0, K % 256 == 0, dense B):
-# ragged rows, one-slice direct stores (K <= 512), a half slice at the end of K, full C3.
-Q32 = [
+# More skinny (2 <= N <= 32) shapes on the product kernels (gemm_skinny_pair_kernel for N > 16):
+# ragged rows, one slice (K <= 512, no split-K reduction), a half slice at the end of K, many tiles
+# per row range.
+SKINNY_EXTRA = [
     (257, 4096, 20),    # ragged rows (a 1-row tile), 8 slices
-    (64, 256, 24),      # one half slice: direct stores
-    (100, 512, 28),     # one full slice: direct stores
+    (64, 256, 24),      # one half slice
+    (100, 512, 28),     # one full slice
     (33, 768, 32),      # a full and a half slice
     (1000, 11008, 32),  # 43 blocks x 8: the last slice half, many tiles per range
 ]
 
 
 @pytest.mark.parametrize("qt", [2, 3], ids=lambda t: QNAME[t])
-@pytest.mark.parametrize("shape", Q32, ids=lambda s: "x".join(map(str, s)))
-def test_q32_gemm_vs_oracle(gpu, oracle, qt, shape, monkeypatch):
-    """gemm_q32_kernel is a lab kernel (LK_Q32=1 routes to it; the library reads the switch once,
-    so this test covers it only when the whole session runs with LK_Q32=1); by default the same
-    shapes run on the skinny kernels."""
+@pytest.mark.parametrize("shape", SKINNY_EXTRA, ids=lambda s: "x".join(map(str, s)))
+def test_skinny_extra_shapes_vs_oracle(gpu, oracle, qt, shape):
     M, K, N = shape
     for kind in ("random", "pattern"):
         q, x = make_inputs(oracle, qt, M, K, N, kind, seed=M + 7 * N)

@@ -158,19 +158,19 @@ def _mul_mat_nodes(G, nodes):
 
 
 def test_backend_writes_back_only_what_leaves_the_graph(gpu, oracle):
-    """The backend keeps results that only later MUL_MATs consume in HBM (q -> o, up -> down);
-    every other result (and anything flagged isOutput) reaches the host bytes, equal to the
-    per-node path bit for bit."""
+    """With wholeGraphs=True the backend keeps results that only later MUL_MATs consume in HBM
+    (q -> o, up -> down); every other result (and anything flagged isOutput) reaches the host
+    bytes, equal to the per-node path bit for bit."""
     import ggml_hip as G
     ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 20)
     _, nodes = _layer(ga, oracle)
     want = _sequential(ga, nodes)
     dsts = _mul_mat_nodes(G, nodes)
-    assert G.backend.writeBackMask(dsts) == [d.name not in ("q", "u") for d in dsts]
+    assert G.backend.writeBackMask(dsts, wholeGraph=True) == [d.name not in ("q", "u") for d in dsts]
     dsts[0].flags = G.tensor.GGML_TENSOR_FLAG_OUTPUT  # q is also wanted by the caller
     for d in dsts:
         ga.setTensorBytes(d, np.zeros(4 * d.ne[1], np.uint8))
-    be = G.GGMLHipBackend(ga)
+    be = G.GGMLHipBackend(ga, wholeGraphs=True)
     assert be.graphCompute(G.GGMLCGraph(dsts, ga)) == G.GGMLStatus.SUCCESS
     for d, w in zip(dsts, want):
         got = bytes(ga.tensorBytes(d))
@@ -222,4 +222,28 @@ def test_backend_weight_generation(gpu, oracle):
     for d, g_, w in zip(dsts, got, want):
         if d.name not in ("q", "u"):
             assert g_ == w, d.name
+    be.free()
+
+
+def test_backend_split_subgraph_results_reach_a_later_cpu_consumer(gpu, oracle):
+    """GGMLScheduler.executeGraphSplit (core/GGMLScheduler.kt:245-258) hands the backend one split
+    of a larger graph and sets no output flags; a CPU node of a later split may read any result
+    (here: ADD(q, o) on the host after the split {q = Wq·x, o = Wo·q}). By default every result of
+    the split reaches the ByteArrays, so the CPU consumer reads q's current bytes."""
+    import ggml_hip as G
+    assert G.backend.writeBackMask([object(), object()]) == [True, True]
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 20)
+    _, nodes = _layer(ga, oracle)
+    split = [nodes[0], nodes[3]]  # q from x, o from q
+    want = _sequential(ga, split)
+    dsts = _mul_mat_nodes(G, split)
+    for d in dsts:
+        ga.setTensorBytes(d, np.zeros(4 * d.ne[1], np.uint8))
+    be = G.GGMLHipBackend(ga)
+    assert be.graphCompute(G.GGMLCGraph(dsts, ga)) == G.GGMLStatus.SUCCESS
+    q = np.frombuffer(bytes(ga.tensorBytes(dsts[0])), np.float32)
+    o = np.frombuffer(bytes(ga.tensorBytes(dsts[1])), np.float32)
+    assert [q.tobytes(), o.tobytes()] == want
+    cpu_add = q + o  # the later split's CPU node
+    assert np.array_equal(cpu_add, np.frombuffer(want[0], np.float32) + np.frombuffer(want[1], np.float32))
     be.free()

@@ -115,3 +115,123 @@ def test_rccl_sharded_plan_rejects_uneven_rows(gpu):
     with pytest.raises(G.IllegalArgumentException):
         G.ShardedMulMatPlan(comm, ga, [(a, b, d)])
     comm.close()
+
+
+def _llama_nodes(G, ga, oracle, shapes, seed=0):
+    """Weights (ne=[K, M]) + activations on device buffers; returns [(a, x, dst)] per shape."""
+    out = []
+    for i, (M, K) in enumerate(shapes):
+        a = ga.allocateTensor(G.GGMLType.Q4_0, [K, M])
+        ga.setTensorBytes(a, oracle.quantize(2, random_weights(M * K, seed + 10 + i)))
+        x = ga.allocateTensor(G.GGMLType.F32, [1, K])
+        ga.setTensorBytes(x, random_acts(K, seed + 20 + i))
+        out.append((a, x, ga.allocateTensor(G.GGMLType.F32, [1, M])))
+    return out
+
+
+def test_rccl_allgather_executes_at_world1_and_replays_in_a_hip_graph(gpu, oracle):
+    """lk_sharded_plan_launch issues its RCCL group at world size 1 too (counted per communicator),
+    and a HIP-graph capture of the launches replays bit-equal to lk_plan — over the Llama-7B shapes,
+    the down projection (4096 x 11008, reading the up projection's gathered output) included."""
+    import torch
+    import ggml_hip as G
+    comm = G.Comm.single()
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 27)
+    (wq, x, dq), (wu, _, du) = _llama_nodes(G, ga, oracle, [(4096, 4096), (11008, 4096)])
+    wd = ga.allocateTensor(G.GGMLType.Q4_0, [11008, 4096])
+    ga.setTensorBytes(wd, oracle.quantize(2, random_weights(4096 * 11008, 77)))
+    dd = ga.allocateTensor(G.GGMLType.F32, [1, 4096])
+    refs = [ga.allocateTensor(G.GGMLType.F32, [1, m]) for m in (4096, 11008, 4096)]
+    plan1 = G.ShardedMulMatPlan(comm, ga, [(G.shard_view(wq, 1, 0), x, dq), (G.shard_view(wu, 1, 0), x, du)])
+    plan2 = G.ShardedMulMatPlan(comm, ga, [(G.shard_view(wd, 1, 0), du, dd)])
+    ref1 = G.MulMatPlan(ga, [(wq, x, refs[0]), (wu, x, refs[1])])
+    ref2 = G.MulMatPlan(ga, [(wd, refs[1], refs[2])])
+    s = torch.cuda.Stream()
+    n0 = comm.numCollectives
+    plan1.launch(stream=s); plan2.launch(stream=s)
+    ref1.launch(stream=s); ref2.launch(stream=s)
+    assert comm.numCollectives == n0 + 3  # one ncclAllGather per node, issued eagerly
+    torch.cuda.synchronize()
+    want = [bytes(ga.tensorBytes(r).cpu().numpy()) for r in refs]
+    assert [bytes(ga.tensorBytes(d).cpu().numpy()) for d in (dq, du, dd)] == want
+    for d in (dq, du, dd):
+        ga.buffers[d.bufferId][d.dataOffset:d.dataOffset + 4 * d.ne[1]].zero_()
+    torch.cuda.synchronize()
+    hg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(hg, stream=s):
+        plan1.launch(stream=s); plan2.launch(stream=s)
+    assert comm.numCollectives == n0 + 6  # captured
+    for _ in range(3):
+        hg.replay()
+    torch.cuda.synchronize()
+    assert [bytes(ga.tensorBytes(d).cpu().numpy()) for d in (dq, du, dd)] == want
+    ok, msg = parity_ok(ga.tensorBytes(dd).cpu().numpy().view(np.float32).reshape(4096, 1),
+                        oracle.mat_mul_q(2, oracle.quantize(2, random_weights(4096 * 11008, 77)), 4096, 11008,
+                                         ga.tensorBytes(du).cpu().numpy().view(np.float32).reshape(11008, 1), tight=True))
+    assert ok, msg
+    del hg
+    plan1.close(); plan2.close(); comm.close()
+
+
+def _host_layer(G, ga, oracle, K=512, F=768, seed=0):
+    """A Llama-style block on host buffers: q,k,v,gate,up from x; o from q; down from up."""
+    x = ga.allocateTensor(G.GGMLType.F32, [1, K], name="x")
+    ga.setTensorBytes(x, random_acts(K, seed + 1))
+    nodes = []
+
+    def node(name, qt, src, k, m, s):
+        w = ga.allocateTensor(G.GGMLType(qt), [k, m], name="w" + name)
+        ga.setTensorBytes(w, oracle.quantize(qt, random_weights(k * m, s)))
+        d = ga.allocateTensor(G.GGMLType.F32, [1, m], name=name)
+        nodes.append((w, src, d))
+        return d
+
+    q = node("q", 2, x, K, K, seed + 2)
+    node("k", 3, x, K, K, seed + 3)
+    node("v", 6, x, K, K, seed + 4)
+    node("o", 2, q, K, K, seed + 5)
+    node("g", 2, x, K, F, seed + 6)
+    u = node("u", 2, x, K, F, seed + 7)
+    node("d", 2, u, F, K, seed + 8)
+    return nodes
+
+
+@pytest.mark.parametrize("mode", ["rank", "init_all", "backend"])
+def test_rccl_sharded_graph_equals_graph(gpu, oracle, mode):
+    """lk_graph_create_sharded over the one GPU (a one-rank communicator from lk_comm_init_rank, or
+    lk_comm_init_all over [0], or GGMLHipBackend(shardDevices=[0])): every weight node runs through a
+    sharded plan and its in-place RCCL all-gather, and every result equals lk_graph's bit for bit,
+    over repeated computes (eager, then HIP-graph replay)."""
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 22)
+    nodes = _host_layer(G, ga, oracle)
+    plain = G.ResidentGraph(ga, nodes)
+    plain.compute()
+    want = [bytes(ga.tensorBytes(d)) for _, _, d in nodes]
+    for _, _, d in nodes:
+        ga.setTensorBytes(d, np.zeros(4 * d.ne[1], np.uint8))
+    if mode == "backend":
+        dsts = []
+        for a, b, d in nodes:
+            d.op, d.src = G.GGMLOp.MUL_MAT, [a, b]
+            dsts.append(d)
+        be = G.GGMLHipBackend(ga, shardDevices=[0])
+        for _ in range(3):
+            assert be.graphCompute(G.GGMLCGraph(dsts, ga)) == G.GGMLStatus.SUCCESS
+            assert [bytes(ga.tensorBytes(d)) for _, _, d in nodes] == want
+        assert be.comms[0].numCollectives >= len(nodes)
+        be.close()
+        return
+    comms = [G.Comm.single()] if mode == "rank" else G.Comm.init_all([0])
+    g = G.ResidentGraph(ga, nodes, comms=comms)
+    assert g.numSharded == len(nodes) and g.numLevels == plain.numLevels
+    n0 = comms[0].numCollectives
+    for i in range(3):
+        g.compute()
+        assert [bytes(ga.tensorBytes(d)) for _, _, d in nodes] == want, i
+        for _, _, d in nodes:
+            ga.setTensorBytes(d, np.zeros(4 * d.ne[1], np.uint8))
+    assert comms[0].numCollectives >= n0 + len(nodes)
+    g.close(); plain.close()
+    for c in comms:
+        c.close()
