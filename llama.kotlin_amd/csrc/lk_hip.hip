@@ -413,6 +413,12 @@ int fused_rsync(int slices, size_t slab_bytes, unsigned **out) {
   return LK_OK;
 }
 
+// Activation fragments for the batched kernels (xsplit_kernel: one wave per x-tile and block).
+void launch_xsplit(const XSplitArgs &xa, hipStream_t st) {
+  const int64_t ntx = (xa.N + 15) / 16, nblk = xa.K / 32;
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+}
+
 int grow(void **p, size_t *have, size_t want) {
   if (*have >= want) return LK_OK;
   if (*p) HIP_TRY(hipFree(*p));
@@ -468,8 +474,7 @@ int launch_gemm_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
     g.partial = (float *)S.partial;
     g.counter = S.counter;
   }
-  const int64_t ntx = (g.N + 15) / 16;
-  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  launch_xsplit(xa, st);
   hipLaunchKernelGGL((gemm_q_mfma_kernel<QT, WM, WN, MT, NT>), dim3((unsigned)(tiles * slices)), dim3(256), 0, st, g);
   HIP_TRY(hipGetLastError());
   return LK_OK;
@@ -515,8 +520,7 @@ int launch_gemm_lds_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
     g.partial = (float *)S.partial;
     g.counter = S.counter;
   }
-  const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
-  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  launch_xsplit(xa, st);
   constexpr size_t lds = GG::LDS;
   hipLaunchKernelGGL((gemm_q_lds_kernel<QT, NT, NW>), dim3((unsigned)(tiles * slices)), dim3(NW * 64), lds, st, g);
   HIP_TRY(hipGetLastError());
@@ -661,7 +665,7 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   g.rsync = rsync;
   g.b = xa.b;
   g.fx = b->nb[0] == 4 && b->nb[1] == 4 * (uint64_t)c.N && ((uintptr_t)xa.b & 15) == 0;
-  if (!g.fx) hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  if (!g.fx) launch_xsplit(xa, st);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_sk_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
   if (slices > 1 && !rsync) {
@@ -711,7 +715,11 @@ bool wide_eligible(const lk_tensor *a, const Checked &c) {
 }
 
 template <int QT>
-int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
+int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
+  if (QT == LK_TYPE_Q4_0) {  // codes 128 + n against activations in k order (0,4,1,5,...), T = −136·Σ(hi + lo)
+    xa.q4_order = 2;
+    xa.mult = -136.f;
+  }
   using WG = WideGeom<QT>;
   GemmScratch &S = gemm_scratch();
   g.tiles_m = (g.M + WG::BM - 1) / WG::BM;
@@ -742,12 +750,11 @@ int launch_wide_t(WideArgs g, const XSplitArgs &xa, hipStream_t st) {
   g.sm = std::min(g.tiles_m, (per_xcd + best - 1) / best);
   const int nsuper = ((g.tiles_m + g.sm - 1) / g.sm) * ((g.tiles_n + g.sn - 1) / g.sn);
   g.tasks = nsuper * g.sm * g.sn * slices;
-  const int64_t ntx = (g.N + 15) / 16, nblk = g.K / 32;
   // fused split-K reduction in gemm_wide_kernel when every task is co-resident (one per CU)
   g.rsync = nullptr;
   if (g.tasks <= cu_count())
     if (int rf = fused_rsync(slices, (size_t)slices * g.M * npad * sizeof(float), &g.rsync)) return rf;
-  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  launch_xsplit(xa, st);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
   if (slices > 1 && !g.rsync) {

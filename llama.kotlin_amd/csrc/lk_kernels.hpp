@@ -990,6 +990,18 @@ __global__ __launch_bounds__(256) void xsplit_kernel(XSplitArgs g) {
   if (lane < 16) g.xsum[kb * (ntx * 16) + n] = g.mult * part;
 }
 
+// bf16 codes 128 + n of the 8 nibbles of dword u, slots in k order (0,4,1,5,2,6,3,7).
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(o));  // one VALU (the compiler splits it)
+  return r;
+}
+__device__ __forceinline__ bf16x8 q4_codes_128(uint32_t u) {
+  constexpr uint32_t M = 0x000F000Fu, E = 0x43004300u;
+  uint32_t w[4] = {and_or(u, M, E), and_or(u >> 4, M, E), and_or(u >> 8, M, E), and_or(u >> 12, M, E)};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 // two f32 whose values fit in 8 significant bits -> their exact bf16 pair (lo, hi)
 __device__ __forceinline__ uint32_t pack_bf16_exact(float lo, float hi) {
   return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07060302u);
@@ -1844,7 +1856,7 @@ template <int QT, int NT> struct SkinnyPairGeom {
   static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
   static constexpr int SLOT = L * 1024;
   static constexpr int XB = SB * NT * kXSplits * 1024;  // activation fragments (staging)
-  static constexpr int TB = QT == LK_TYPE_Q4_1 ? SB * NT * 16 * 4 : 0;  // Σx per (block, column)
+  static constexpr int TB = QT == LK_TYPE_Q8_0 ? 0 : SB * NT * 16 * 4;  // Q4_1 Σx / Q4_0 −136·Σ(hi+lo) per (block, column)
   static constexpr int EB = 2 * 4 * NT * 64 * 16;       // accumulator hand-off, 2 parities x 4 pairs
   static constexpr int FB = 64;                         // ready[4][2], ack[4] (ints)
   static constexpr int DFIT = (kLdsBytes - XB - TB - EB - FB) / (NW * SLOT);
@@ -1892,13 +1904,13 @@ __device__ __forceinline__ void skinny_pair_block(const uint32_t (&w)[WPB], cons
     wf = Q4Frag<0>::make(w[1]);
     s1 = 512.f * h2f(w[0]);
     s2 = h2f(w[0] >> 16);
-  } else if constexpr (QT == LK_TYPE_Q4_0) {
+  } else if constexpr (QT == LK_TYPE_Q4_0) {  // codes 128 + n; −136·Σx enters as the MFMA's C (T)
     if constexpr ((OB & 3) == 0) {
-      wf = q4_0_frag_biased(align2(w[2], w[1]));
-      s1 = 512.f * h2f(w[0]);
+      wf = q4_codes_128(align2(w[2], w[1]));
+      s1 = h2f(w[0]);
     } else {
-      wf = q4_0_frag_biased(w[1]);
-      s1 = 512.f * h2f(w[0] >> 16);
+      wf = q4_codes_128(w[1]);
+      s1 = h2f(w[0] >> 16);
     }
   } else {
     if constexpr ((OB & 3) == 0) {
@@ -1911,15 +1923,15 @@ __device__ __forceinline__ void skinny_pair_block(const uint32_t (&w)[WPB], cons
   }
 #pragma unroll
   for (int j = 0; j < NT; j++) {
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (QT != LK_TYPE_Q8_0) t = *(const f32x4 *)(tl + (B * NT + j) * 16 + (lane >> 4) * 4);
 #if LK_SKP_SKEL == 1
     f32x4 p = __builtin_bit_cast(f32x4, wf);
 #else
-    f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf, f32x4{0.f, 0.f, 0.f, 0.f},
-                                                      0, 0, 0);
+    f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf,
+                                                      QT == LK_TYPE_Q4_0 ? t : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
 #endif
-    f32x4 t = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (QT == LK_TYPE_Q4_1) t = *(const f32x4 *)(tl + (B * NT + j) * 16 + (lane >> 4) * 4);
     accumulate_s<QT == LK_TYPE_Q4_1>(acc[j], s1, s2, p, t);
   }
 }
@@ -2038,14 +2050,15 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     const bool ok = b < nb && n < g.N;
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      const int kk = (QT != LK_TYPE_Q8_0) ? ((e & 3) * 2 + (e >> 2)) : e;
+      // k order within 8: Q4_0 (0,4,1,5,2,6,3,7) for q4_codes_128, Q4_1 (0,2,4,6,1,3,5,7) for Q4Frag
+      const int kk = QT == LK_TYPE_Q4_0 ? ((e >> 1) + 4 * (e & 1)) : QT == LK_TYPE_Q4_1 ? ((e & 3) * 2 + (e >> 2)) : e;
       v[i][e] = ok ? *(const float *)(g.b + n * g.b_nb0 + (k0 + kk) * g.b_nb1) : 0.f;
     }
   }
 #pragma unroll
   for (int i = 0; i < G::FPW; i++) {
     const int f = wave + i * NW;
-    float part = 0.f;
+    float part = 0.f, hsum = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; e++) part += v[i][e];
     uint32_t hi[4], lo[4];
@@ -2060,6 +2073,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
         br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even
         hh[q] = bx;
         ll[q] = br;
+        // Q4_0's −136·Σx cancels against Σ (128 + n)·(hi + lo): sum the split itself, so the
+        // split's own error is not amplified
+        hsum += __builtin_bit_cast(float, bx & 0xFFFF0000u) + __builtin_bit_cast(float, br & 0xFFFF0000u);
       }
       hi[e / 2] = __builtin_amdgcn_perm(hh[1], hh[0], 0x07060302u);
       lo[e / 2] = __builtin_amdgcn_perm(ll[1], ll[0], 0x07060302u);
@@ -2067,10 +2083,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     u32x4 *xf = (u32x4 *)(xlds + (f * kXSplits) * 1024) + lane;
     xf[0] = u32x4{hi[0], hi[1], hi[2], hi[3]};
     xf[64] = u32x4{lo[0], lo[1], lo[2], lo[3]};
-    if constexpr (QT == LK_TYPE_Q4_1) {
+    if constexpr (QT != LK_TYPE_Q8_0) {
+      if constexpr (QT == LK_TYPE_Q4_0) part = hsum;
       part += __shfl_xor(part, 16, kWave);
       part += __shfl_xor(part, 32, kWave);
-      if (lane < 16) tlds[f * 16 + lane] = part;
+      if (lane < 16) tlds[f * 16 + lane] = QT == LK_TYPE_Q4_0 ? -136.f * part : part;
     }
   }
   LK_PTRACE(1);
@@ -2238,13 +2255,23 @@ template <int QT> struct WideGeom {
   static constexpr int WPIECES = BM * WIN / 16;                 // 16-B DMA pieces of weights
   static constexpr int W_INST = (WPIECES + 63) / 64;
   static constexpr int X_INST = SB * NT * kXSplits;             // 1-KB activation fragments
-  static constexpr int T_INST = (QT == LK_TYPE_Q4_1) ? 1 : 0;
-  static constexpr int CWW = (W_INST + NW - 1) / NW, CWX = (X_INST + NW - 1) / NW, CWT = T_INST;
+  static constexpr int T_INST = (QT == LK_TYPE_Q8_0) ? 0 : 1;  // Σx per (block, column): Q4_1 m·Σx, Q4_0 −136·Σx
+  // Weight pieces per wave: the first WX waves issue CWW, the rest CWW − 1. Every wave issues the
+  // same count per stage (a counted vmcnt + one barrier publish a stage), so the spare slot of the
+  // short waves carries T (1 KB = T_PARTS parts of TL lanes, no duplicates) — or, without T
+  // (Q8_0) or when no part shape fits, a padding piece into DUMMY.
+  static constexpr int CWW = (W_INST + NW - 1) / NW, CWX = (X_INST + NW - 1) / NW;
+  static constexpr int WX = W_INST % NW;
+  static constexpr int T_PARTS = WX ? NW - WX : 0;
+  static constexpr bool T_SPARE = T_INST && WX && 64 % (NW - WX) == 0;
+  static constexpr int TL = T_SPARE ? 64 / T_PARTS : 64;
+  static constexpr int CWT = T_INST && !T_SPARE ? 1 : 0;         // else: T by every wave (same 1 KB)
   static constexpr int CW = CWW + CWX + CWT;                    // DMA instructions per wave per stage
-  static constexpr int W_BYTES = W_INST * 1024;   // padding instructions (CWW·NW - W_INST) land in DUMMY
+  static constexpr int W_BYTES = W_INST * 1024;
   static constexpr int X_BYTES = X_INST * 1024;
   static constexpr int T_OFF = W_BYTES + X_BYTES, DUMMY = T_OFF + (T_INST ? 1024 : 0);
-  static constexpr int STAGE = DUMMY + 1024;
+  static constexpr bool NEED_DUMMY = WX && !T_SPARE;
+  static constexpr int STAGE = DUMMY + (NEED_DUMMY ? 1024 : 0);
 #ifdef LK_WIDE_D
   static constexpr int D = LK_WIDE_D;
 #else
@@ -2257,6 +2284,7 @@ template <int QT> struct WideGeom {
   static_assert(X_INST % NW == 0, "activation pieces per wave");
   static_assert(SB % KG == 0, "blocks per K-group");
   static_assert(MW * MT * NT * 256 * 4 <= D * STAGE, "K-group reduction buffer");
+  static_assert(!T_INST || T_SPARE || CWT, "T");
 };
 
 struct WideArgs {
@@ -2280,6 +2308,9 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the second-dispatched half of the workgroup loses issue arbitration on its SIMD to the first:
+  // static priority for it (MI355X_MICROARCH.md, two waves per SIMD, item 4): C5 ~2 % faster
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   // Task order (speed only: dispatch is observed round-robin over the 8 XCDs): workgroup b runs
   // task (b % 8)·(grid / 8) + b / 8, so each XCD gets a contiguous run of tasks; tasks walk
   // super-tiles of sm row bands x sn column tiles (all slices), so an XCD's L2 holds the
@@ -2299,9 +2330,12 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
 
   // per-lane DMA offsets (fixed for the launch) from each kind's stage base
   uint32_t wofs[G::CWW], xofs[G::CWX], tofs = 0;
+  // this wave's weight instructions: q = wq0 .. wq0 + nwq − 1 (see WideGeom)
+  const int nwq = (G::WX == 0 || wave < G::WX) ? G::CWW : G::CWW - 1;
+  const int wq0 = (G::WX == 0 || wave < G::WX) ? wave * G::CWW : G::WX * G::CWW + (wave - G::WX) * (G::CWW - 1);
 #pragma unroll
   for (int c = 0; c < G::CWW; c++) {
-    const int piece = min((wave * G::CWW + c) * 64 + lane, G::WPIECES - 1);
+    const int piece = min((wq0 + min(c, nwq - 1)) * 64 + lane, G::WPIECES - 1);
     const int r = piece / (G::WIN / 16), pc = piece % (G::WIN / 16);
     const int64_t row = min((int64_t)tm * BM + r, (int64_t)g.M - 1);
     wofs[c] = (uint32_t)(row * RB + pc * 16);
@@ -2314,7 +2348,8 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
     xofs[c] = (uint32_t)((((int64_t)xt * nblk + b) * kXSplits + sp) * 1024 + lane * 16);
   }
   if constexpr (G::T_INST) {
-    const int li = min(lane, SB * BN / 4 - 1);  // lane -> (block li / (BN/4), 4 columns)
+    // lane -> T index li = (block li / (BN/4), 4 columns); a spare-slot part covers TL of them
+    const int li = min((G::T_SPARE ? (wave - G::WX) * G::TL : 0) + lane, SB * BN / 4 - 1);
     const int b = li / (BN / 4), c4 = li % (BN / 4);
     const int n = min(tn * BN + 4 * c4, n16 - 4);
     tofs = (uint32_t)(((int64_t)b * n16 + n) * 4);
@@ -2326,12 +2361,18 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
     uint8_t *slot = smem + sl * G::STAGE;
 #pragma unroll
     for (int c = 0; c < G::CWW; c++) {
-      const int q = wave * G::CWW + c;  // past W_INST: a padding instruction (same count on every wave)
-      dma16<false>(base_a, wofs[c], slot + (q < G::W_INST ? q * 1024 : G::DUMMY));
+      if (c < nwq) {
+        dma16<false>(base_a, wofs[c], slot + (wq0 + c) * 1024);
+      } else if constexpr (G::T_SPARE) {  // T part (wave − WX): TL lanes, TL·16 bytes
+        if (lane < G::TL)
+          dma16<false>((const uint8_t *)(g.xsum + (int64_t)kb * n16), tofs, slot + G::T_OFF + (wave - G::WX) * G::TL * 16);
+      } else {
+        dma16<false>(base_a, wofs[c], slot + G::DUMMY);  // padding (never read)
+      }
     }
 #pragma unroll
     for (int c = 0; c < G::CWX; c++) dma16<false>(base_x, xofs[c], slot + G::W_BYTES + (wave * G::CWX + c) * 1024);
-    if constexpr (G::T_INST)
+    if constexpr (G::CWT)
       dma16<false>((const uint8_t *)(g.xsum + (int64_t)kb * n16), tofs, slot + G::T_OFF);
   };
 
@@ -2357,7 +2398,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
       // this K-group's blocks of the stage into registers with one burst of LDS reads, so the
       // slot can be refilled at once and the MFMAs never wait on LDS
       constexpr int WD = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
-      constexpr bool EARLY = QT != LK_TYPE_Q4_1;  // Q4_1 reads its Σx during the compute
+      constexpr bool EARLY = QT == LK_TYPE_Q8_0;  // Q4_0 / Q4_1 read their Σx during the compute
       uint32_t wd[BPG][MT][WD];
       u32x4 xh[BPG][NT], xl[BPG][NT];
 #pragma unroll
@@ -2420,13 +2461,13 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
             wf[i] = Q4Frag<0>::make(wd[bb][i][1]);
             s1[i] = 512.f * h2f(wd[bb][i][0]);
             s2[i] = h2f(wd[bb][i][0] >> 16);
-          } else if constexpr (QT == LK_TYPE_Q4_0) {
+          } else if constexpr (QT == LK_TYPE_Q4_0) {  // codes 128 + n; −136·Σx enters as the MFMA's C
             if ((bb & 1) == 0) {
-              wf[i] = q4_0_frag_biased(align2(wd[bb][i][2], wd[bb][i][1]));
-              s1[i] = 512.f * h2f(wd[bb][i][0]);
+              wf[i] = q4_codes_128(align2(wd[bb][i][2], wd[bb][i][1]));
+              s1[i] = h2f(wd[bb][i][0]);
             } else {
-              wf[i] = q4_0_frag_biased(wd[bb][i][1]);
-              s1[i] = 512.f * h2f(wd[bb][i][0] >> 16);
+              wf[i] = q4_codes_128(wd[bb][i][1]);
+              s1[i] = h2f(wd[bb][i][0] >> 16);
             }
           } else {
             if ((bb & 1) == 0) {
@@ -2441,11 +2482,12 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
 #pragma unroll
         for (int j = 0; j < NT; j++) {
           f32x4 t = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (QT == LK_TYPE_Q4_1) t = *(const f32x4 *)(T + b * BN + j * 16 + gq * 4);
+          if constexpr (QT != LK_TYPE_Q8_0) t = *(const f32x4 *)(T + b * BN + j * 16 + gq * 4);
 #pragma unroll
           for (int i = 0; i < MT; i++) {
+            // Q4_0: p = Σ (128 + n)·x − 136·Σx = Σ (n − 8)·x (T is −136·Σ(hi + lo), the split's own sum)
             f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[bb][j]), wf[i],
-                                                              f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                                                              QT == LK_TYPE_Q4_0 ? t : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[bb][j]), wf[i], p, 0, 0, 0);
             accumulate<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], p, t);
           }

@@ -139,18 +139,6 @@ __device__ __forceinline__ void sk_read_all(const lu8 *bm, const lu8 *bg, uint32
   }
 }
 
-// bf16 codes 128 + n of the 8 nibbles of dword u, slots in k order (0,4,1,5,2,6,3,7).
-__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
-  uint32_t r;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(o));  // one VALU (the compiler splits it)
-  return r;
-}
-__device__ __forceinline__ bf16x8 q4_codes_128(uint32_t u) {
-  constexpr uint32_t M = 0x000F000Fu, E = 0x43004300u;
-  uint32_t w[4] = {and_or(u, M, E), and_or(u >> 4, M, E), and_or(u >> 8, M, E), and_or(u >> 12, M, E)};
-  return __builtin_bit_cast(bf16x8, w);
-}
-
 // Q4_K block header of the lane's row (per unit): h = its first 16 bytes (d, dmin, 12 scale
 // bytes), dk = d/945 (= d/63/15). Sub-block sb's weights are w = (q/15)·scale + min with
 // scale = (qs/63)·d, min = (qm/63)·d + dmin (:285-286, :298): here as the affine q·s1 + min with

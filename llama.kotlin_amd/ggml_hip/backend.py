@@ -19,7 +19,7 @@ from collections import OrderedDict
 
 from . import _lib
 from .ops import MulMatPlan, ResidentGraph, _is_host, computeMatMul
-from .tensor import GGMLCGraph, GGMLOp, GGMLTensor, GGMLType
+from .tensor import GGMLCGraph, GGMLOp, GGMLTensor, GGMLType, descriptorEpoch
 
 
 class GGMLStatus(enum.Enum):
@@ -152,6 +152,8 @@ class GGMLHipBackend:
         self.weightGeneration = 0
         self.wholeGraphs = wholeGraphs
         self._plans: "OrderedDict[tuple, object]" = OrderedDict()
+        # fast path: (graph, allocator, node identities, descriptor epoch, ...) -> full plan key
+        self._fast: dict = {}
         self.comms = None
         if shardDevices:
             from .sharded import Comm
@@ -167,6 +169,7 @@ class GGMLHipBackend:
         for p in self._plans.values():
             p.close()
         self._plans.clear()
+        self._fast.clear()
 
     def close(self):
         """free() plus the communicators (after every graph that uses them)."""
@@ -242,6 +245,14 @@ class GGMLHipBackend:
         ga = graph.allocator or self.graphAllocator
         try:
             nodes = [n for n in graph.nodes[: graph.nNodes] if n is not None and n.op != GGMLOp.NONE]
+            # fast path: the same node objects, no descriptor changed since (tensor.descriptorEpoch),
+            # the same buffers and weight generation: the cached graph's key without rebuilding it
+            fast = (id(graph), id(ga), descriptorEpoch(), self.weightGeneration, _buffer_table(ga), tuple(map(id, nodes)))
+            key = self._fast.get(fast)
+            if key is not None and key in self._plans:
+                self._plans.move_to_end(key)
+                self._plans[key].compute()
+                return GGMLStatus.SUCCESS
             for n in nodes:
                 if not self.supportsOp(n):
                     raise _lib.NotOffloadedError(f"node {n.name!r} ({n.op}) is not supported by the HIP backend")
@@ -252,6 +263,9 @@ class GGMLHipBackend:
                 key = ("host", self.weightGeneration, id(ga), _graph_key(ga, nodes, mask))
                 g = self._cached(key, lambda: ResidentGraph(ga, [(n.src[0], n.src[1], n) for n in nodes], outputs=mask,
                                                             weightGeneration=self.weightGeneration, comms=self.comms))
+                if len(self._fast) > 4 * self.MAX_CACHED_GRAPHS:
+                    self._fast.clear()
+                self._fast[fast] = key
                 g.compute()
                 return GGMLStatus.SUCCESS
             ids = {id(n) for n in nodes}

@@ -96,9 +96,84 @@ def calculateContiguousStrides(ne, type_: GGMLType, rank: int | None = None):
 
 GGML_TENSOR_FLAG_OUTPUT = 1 << 0  # core/GGMLTypes.kt:83
 
+# Descriptor epoch: bumped whenever any GGMLTensor's type / ne / nb / bufferId / dataOffset / op /
+# src / flags is assigned or mutated in place, or a tensor is created. A backend that cached work
+# for a set of descriptors at epoch e knows nothing it baked in changed while the epoch is still e
+# (GGMLHipBackend.graphCompute's fast path); any change sends it back to the full comparison.
+_desc_epoch = [0]
+_DESC_FIELDS = frozenset(("type", "ne", "nb", "bufferId", "dataOffset", "op", "src", "flags"))
+
+
+def descriptorEpoch() -> int:
+    return _desc_epoch[0]
+
+
+class _Tracked(list):
+    """A list whose in-place mutations bump the descriptor epoch (GGMLTensor.ne / nb / src)."""
+
+    __slots__ = ()
+
+    def _bump(self):
+        _desc_epoch[0] += 1
+
+    def __setitem__(self, i, v):
+        self._bump()
+        super().__setitem__(i, v)
+
+    def __delitem__(self, i):
+        self._bump()
+        super().__delitem__(i)
+
+    def __iadd__(self, other):
+        self._bump()
+        return super().__iadd__(other)
+
+    def __imul__(self, n):
+        self._bump()
+        return super().__imul__(n)
+
+    def append(self, v):
+        self._bump()
+        super().append(v)
+
+    def extend(self, v):
+        self._bump()
+        super().extend(v)
+
+    def insert(self, i, v):
+        self._bump()
+        super().insert(i, v)
+
+    def pop(self, *a):
+        self._bump()
+        return super().pop(*a)
+
+    def remove(self, v):
+        self._bump()
+        super().remove(v)
+
+    def clear(self):
+        self._bump()
+        super().clear()
+
+    def sort(self, *a, **k):
+        self._bump()
+        super().sort(*a, **k)
+
+    def reverse(self):
+        self._bump()
+        super().reverse()
+
 
 class GGMLTensor:
     """core/GGMLTypes.kt:251-270 — a descriptor; bytes live in graphAllocator.buffers[bufferId]."""
+
+    def __setattr__(self, name, value):
+        if name in _DESC_FIELDS:
+            _desc_epoch[0] += 1
+            if name in ("ne", "nb", "src") and value is not None and not isinstance(value, _Tracked):
+                value = _Tracked(value)
+        object.__setattr__(self, name, value)
 
     def __init__(self, type=GGMLType.F32, ne=None, nb=None, name: str = "", bufferId: int = -1,
                  dataOffset: int = 0, op: GGMLOp = GGMLOp.NONE, src=None, flags: int = 0):

@@ -40,7 +40,7 @@ def test_wait_that_gives_up_raises(gpu, oracle):
     want = gpu_matmul(qt, q, M, K, N, x, host=True)
     ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=q.size + 4 * (K * N + M * N) + 4096)
     a = ga.allocateTensor(G.GGMLType.Q4_0, [K, M]); ga.setTensorBytes(a, q)
-    b = ga.allocateTensor(G.GGMLType.F32, [N, K]); ga.setTensorBytes(b, np.ascontiguousarray(x.T))
+    b = ga.allocateTensor(G.GGMLType.F32, [N, K]); ga.setTensorBytes(b, np.ascontiguousarray(x))  # B(n, k) at k*4N + 4n
     d = ga.allocateTensor(G.GGMLType.F32, [N, M])
     g = G.ResidentGraph(ga, [(a, b, d)])
     g.compute()
