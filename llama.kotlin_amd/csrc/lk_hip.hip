@@ -413,10 +413,10 @@ int fused_rsync(int slices, size_t slab_bytes, unsigned **out) {
   return LK_OK;
 }
 
-// Activation fragments for the batched kernels (xsplit_kernel: one wave per x-tile and block).
+// Activation fragments for the batched kernels (xsplit_kernel: a wave per kXsItems (x-tile, block) items).
 void launch_xsplit(const XSplitArgs &xa, hipStream_t st) {
-  const int64_t ntx = (xa.N + 15) / 16, nblk = xa.K / 32;
-  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  const int64_t ntx = (xa.N + 15) / 16, nblk = xa.K / 32, waves = (ntx * nblk + kXsItems - 1) / kXsItems;
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, xa);
 }
 
 int grow(void **p, size_t *have, size_t want) {
@@ -1447,20 +1447,27 @@ const bool g_straddle = [] {
   return e && *e == '1';
 }();
 
-void split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<std::vector<StreamWork>> &per) {
+// Whole nodes per workgroup when there are workgroups enough: node i gets a share wg[i] of the
+// grid proportional to its bytes (largest remainder, at least one), its rows split evenly over
+// them (workgroup k of the node: rows [M·k/wg, M·(k+1)/wg)). A workgroup then runs ONE segment:
+// no second prologue (activation image, ring refill) behind a workgroup barrier halfway through,
+// which left the straddling workgroups ~3 µs behind the rest of a Llama-7B layer launch. The byte
+// imbalance the rounding leaves is under 1 % on the Llama shapes. One node: the whole grid.
+// False when the grid is too small for whole nodes (or LK_STRADDLE=1): split_rows then cuts
+// the concatenated rows by bytes.
+bool whole_node_shares(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<int> &wg) {
   const int64_t pb = stream_pair_bytes(qt);
   const size_t n = descs.size();
-  // Whole nodes per workgroup when there are workgroups enough: node i gets a share of the grid
-  // proportional to its bytes (largest remainder, at least one), its rows split evenly over
-  // them. A workgroup then runs ONE segment: no second prologue (activation image, ring refill)
-  // behind a workgroup barrier halfway through, which left the straddling workgroups ~3 µs
-  // behind the rest of a Llama-7B layer launch. The byte imbalance the rounding leaves is
-  // under 1 % on the Llama shapes.
+  if (n == 1) {
+    wg.assign(1, (int)std::min<int64_t>(grid, std::max<int64_t>(1, descs[0].M)));
+    return !g_straddle;
+  }
   int64_t all_bytes = 0;
   std::vector<int64_t> nbytes(n);
   for (size_t i = 0; i < n; i++) all_bytes += nbytes[i] = (int64_t)descs[i].M * (descs[i].K / 64) * pb;
-  if (!g_straddle && n > 1 && (int)n <= grid / 2 && all_bytes > 0) {
-    std::vector<int> wg(n);
+  if (g_straddle || (int)n > grid / 2 || all_bytes <= 0) return false;
+  {
+    wg.assign(n, 0);
     std::vector<std::pair<double, size_t>> rem;
     int used = 0;
     for (size_t i = 0; i < n; i++) {
@@ -1482,6 +1489,15 @@ void split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::v
       for (size_t i = 1; i < n; i++) if (wg[i] > wg[w]) w = i;
       wg[w]--; used--;
     }
+  }
+  return true;
+}
+
+void split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<std::vector<StreamWork>> &per) {
+  const int64_t pb = stream_pair_bytes(qt);
+  const size_t n = descs.size();
+  std::vector<int> wg;
+  if (whole_node_shares(descs, qt, grid, wg)) {
     per.assign(grid, {});
     int g = 0;
     for (size_t i = 0; i < n; i++) {

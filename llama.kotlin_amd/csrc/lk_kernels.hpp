@@ -266,34 +266,10 @@ __global__ __launch_bounds__(256) void gemv_q_n1_kernel(const GemvDesc d) {
 typedef float f2v __attribute__((ext_vector_type(2)));
 #define LK_LDS __attribute__((address_space(3)))
 
-// Cache policy (aux) of the weight stream's LDS-DMA: 2 = nt (bytes read once per launch).
-#ifndef LK_WEIGHT_AUX
-#define LK_WEIGHT_AUX 2
-#endif
-// Prologue order: 0 = activations then D weight units; 1 = weight unit 0, activations, units 1..D-1;
-// 2 = activations, wait for them, then the D weight units.
-#ifndef LK_EARLY_ISSUE
-#define LK_EARLY_ISSUE 1  // refill a slot before decoding it (+0.7 % on the layer launch)
-#endif
-#ifndef LK_STREAM_BIAS
-#define LK_STREAM_BIAS 500  // per mille of a workgroup's rows taken by waves 0..3
-#endif
-#ifndef LK_STREAM_D
-#define LK_STREAM_D 3  // weight units in flight per wave (capped by LDS)
-#endif
-// Lab: LK_STREAM_DYN = c > 0 hands a workgroup's rows to its waves at run time,
-// c units' worth per grab of an LDS counter (after a static first share that covers each wave's
-// prologue), instead of a fixed eighth per wave. The waves then finish together, but the layer
-// launch is slower (26.8-31.0 vs 24.6-25.8 us), so the product keeps the fixed split.
-#ifndef LK_STREAM_DYN
-#define LK_STREAM_DYN 0
-#endif
-#ifndef LK_TIGHT_SLOTS
-#define LK_TIGHT_SLOTS 0
-#endif
-#ifndef LK_PROLOGUE_ORDER
-#define LK_PROLOGUE_ORDER 0
-#endif
+// The weight stream's LDS-DMA uses cache policy nt (aux 2: bytes read once per launch). The
+// prologue issues the activation image, then the ring's D weight units. Rows are split over the
+// workgroup's waves statically (an eighth each): handing rows out at run time evened the waves'
+// exits but made the layer launch slower (26.8-31.0 vs 24.6-25.8 us).
 
 constexpr int kStreamWaves = 8;
 constexpr int kLdsBytes = 160 * 1024;
@@ -315,6 +291,7 @@ struct StreamWork {
   unsigned *sync;
 };
 static_assert(sizeof(StreamWork) == 64, "one s_load_dwordx16");
+
 constexpr int kChainLine = 32;  // chain sync words: one per 128-B line
 
 // Device-side waits (the fused split-K reductions, the chain plans' grid barriers) are bounded:
@@ -345,18 +322,14 @@ template <int QT, int CPL> struct StreamGeom {
   static constexpr int PDW = PB / 4;
   static constexpr int UB = 64 * PB;                      // bytes per unit
   static constexpr int L = (UB + 1023) / 1024;            // DMA instructions per unit
-  // LK_TIGHT_SLOTS: a slot is the unit's own bytes (the last DMA instruction's lanes past the
-  // unit are masked off) instead of L KB, so more units fit in flight
-  static constexpr int SLOT = LK_TIGHT_SLOTS ? (UB + 15) / 16 * 16 : L * 1024;
+  static constexpr int SLOT = L * 1024;                   // a ring slot: the unit's DMA instructions
   static constexpr int IMG = 64 * CPL * 256;              // activation image: 256 B per pair
-  // LK_STREAM_DYN: row queues (8 x 8 words) + the row counter; Q4_K: the table i/63 (64 floats)
   static constexpr bool KQ = QT == LK_TYPE_Q4_K || QT == LK_TYPE_Q2_K;
-  static constexpr int AUX = (LK_STREAM_DYN ? 512 : 0) + (KQ ? 256 : 0);
+  static constexpr int AUX = KQ ? 256 : 0;                // K-quants: the i/63 (Q4_K) or i/15 (Q2_K) table
   static constexpr int DFIT = (kLdsBytes - IMG - AUX) / (kStreamWaves * SLOT);
-  static constexpr int D = DFIT < LK_STREAM_D ? DFIT : LK_STREAM_D;  // ring depth (units)
-  static constexpr int QOFF = IMG + kStreamWaves * D * SLOT;  // LK_STREAM_DYN: wave w's queue at QOFF + 32w, counter at QOFF + 256
-  static constexpr int TOFF = QOFF + (LK_STREAM_DYN ? 512 : 0);  // K-quants: the i/63 (Q4_K) or i/15 (Q2_K) table
-  static constexpr int LDS = QOFF + AUX;
+  static constexpr int D = DFIT < 3 ? DFIT : 3;           // ring depth (units in flight per wave)
+  static constexpr int TOFF = IMG + kStreamWaves * D * SLOT;
+  static constexpr int LDS = TOFF + AUX;
   static constexpr int VMCNT = (D - 1) * L;               // DMA ops allowed in flight past the unit in use
   static_assert(D >= 2, "ring must double-buffer");
   static_assert(VMCNT < 64, "vmcnt field is 6 bits");
@@ -462,23 +435,9 @@ __device__ float q4k_stream_dot(const u32x4 &h, const u32x4 &c0, const u32x4 &c1
 __device__ float q2k_stream_dot(uint32_t sc, const uint32_t *c, uint32_t dd, const f32x4 *xr, const float *xq,
                                 const float *q15);
 
-// Optional per-wave timeline (tools/lab/trace.hip defines LK_STREAM_TRACE): s_memrealtime
-// (100 MHz) at kernel entry, activations in VGPRs, first unit decoded, and exit.
-#ifdef LK_STREAM_TRACE
-__device__ uint64_t *lk_trace_buf;
-// the buffer pointer comes from a scalar load (a vector load would wait behind the DMA)
-#define LK_TRACE(slot)                                                                                  \
-  do {                                                                                                  \
-    uint64_t *tb_ = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_trace_buf)[0]; \
-    if (lane == 0 && tb_)                                                                               \
-      tb_[((size_t)blockIdx.x * kStreamWaves + wave) * 4 + (slot)] = __builtin_amdgcn_s_memrealtime();  \
-  } while (0)
-#else
-#define LK_TRACE(slot) do {} while (0)
-#endif
-
-// Grid: one workgroup per CU. work == nullptr: one node (`single`), rows split evenly
-// over the grid; otherwise workgroup g runs its slots of `work`.
+// Grid: one workgroup per CU. args.work == nullptr: the nodes of args.node (workgroups
+// [wg0, wg0 + nwg) per node, rows split evenly over them); otherwise workgroup g runs its slots
+// of args.work (chain plans).
 // Requirements (checked by the host): K % 64 == 0, ceil(K/4096) <= CPL, row bytes
 // (K/64·PB) % 16 == 0, A and x 16-byte aligned, x contiguous.
 template <int QT, int CPL>
@@ -494,7 +453,6 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     if (tid < 64) q63[tid] = __fdiv_rn((float)tid, 63.0f);
   if constexpr (QT == LK_TYPE_Q2_K)
     if (tid < 16) q63[tid] = __fdiv_rn((float)tid, 15.0f);
-  LK_TRACE(0);
   const StreamWork *wk = work ? work + (int64_t)blockIdx.x * spw : nullptr;
   const int nseg = wk ? ((const __attribute__((address_space(4))) int32_t *)wk)[offsetof(StreamWork, count) / 4] : 1;
   int nbar = 0;
@@ -527,48 +485,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     const int NP = K >> 6;                         // block pairs per row
     const int nch = (NP + 63) >> 6;                // units per row
     const int64_t RB = (int64_t)NP * G::PB;        // row bytes
-#if LK_STREAM_DYN
-    // rows are relative to rb. Wave w first takes rows [w·S, w·S + S) (S rows hold the D units of
-    // its prologue, issued before the barrier that publishes the counter), then one row per grab
-    // of the LDS counter (first value 8·S). A wave's rows are decoded in the order it took them:
-    // their indices wait in its 8-entry LDS queue between the DMA issue and the store.
-    const int R = re - rb;
-    // (a range too short for 8 such shares is split evenly, the counter then starts past it)
-    const int SD = (G::D + nch - 1) / nch;
-    const int S = R >= kStreamWaves * SD ? SD : (R + kStreamWaves - 1) / kStreamWaves;
-    const int s0 = __builtin_amdgcn_readfirstlane(min(wave * S, R));
-    int s_end = __builtin_amdgcn_readfirstlane(min(s0 + S, R));  // end of the wave's current run of rows
-    const int CR = LK_STREAM_DYN > nch ? LK_STREAM_DYN / nch : 1;    // rows per grab
-    const int r0 = rb, row_first = s0;
-    const int nunits = (s_end - s0) * nch;         // units the prologue issues for real
-    LK_LDS int *rowq = (LK_LDS int *)((uint8_t *)lds + G::QOFF) + wave * 8;
-    LK_LDS unsigned *rctr = (LK_LDS unsigned *)((uint8_t *)lds + G::QOFF + 256);
-    int qn = 0;                                    // rows taken (pushed on the queue)
-    bool pending = false, exhausted = false;       // the next row must come from the counter / none left
-    auto push = [&](int r) __attribute__((always_inline)) {
-      if (lane == 0) rowq[qn & 7] = r;
-      ++qn;
-    };
-    auto init_ctr = [&]() __attribute__((always_inline)) {
-      if (wave == 0 && lane == 0) *rctr = (unsigned)(kStreamWaves * S);
-    };
-    if (s0 < s_end) push(s0);
-#else
-#if LK_STREAM_BIAS == 500
     const int per_w = (re - rb + kStreamWaves - 1) / kStreamWaves;
     const int r0 = __builtin_amdgcn_readfirstlane(min(rb + wave * per_w, re));
     const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + per_w, re) - r0);
-#else
-    // waves 0..3 take LK_STREAM_BIAS/1000 of the rows (lab: uneven split between SIMD partners)
-    const int R = re - rb, Ra = (int)((int64_t)R * LK_STREAM_BIAS / 1000);
-    const int pa = (Ra + 3) / 4, pb = (R - min(4 * pa, R) + 3) / 4;
-    const int beg = wave < 4 ? rb + wave * pa : min(rb + 4 * pa, re) + (wave - 4) * pb;
-    const int r0 = __builtin_amdgcn_readfirstlane(min(beg, re));
-    const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + (wave < 4 ? pa : pb), re) - r0);
-#endif
-    const int nunits = nrows * nch, row_first = 0;
-    auto init_ctr = [&]() __attribute__((always_inline)) {};
-#endif
+    const int nunits = nrows * nch;
     const LK_GLOBAL uint8_t *A = (const LK_GLOBAL uint8_t *)a_node + (int64_t)r0 * RB;
 
     // 1. prologue, all by LDS-DMA:
@@ -578,18 +498,13 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     //      (XOR swizzle: each DMA instruction reads 1 KB of x contiguously, and the per-lane
     //      reads below hit 64 distinct banks); image float4 i = 64·k + lane comes from DMA
     //      instruction k, issued by wave k % 8.
-    //    LK_PROLOGUE_ORDER 1 issues weight unit 0 first, then the image, then units 1..D-1:
+    //    0 1 issues weight unit 0 first, then the image, then units 1..D-1:
     //    the HBM stream starts at once and the wait for the image covers unit 0 too.
-    int irow = row_first, ich = 0, islot = 0, issued = 0;
+    int irow = 0, ich = 0, islot = 0, issued = 0;
     auto advance = [&]() __attribute__((always_inline)) {  // past an issued unit
       if (++ich == nch) {
         ich = 0;
-#if LK_STREAM_DYN
-        if (irow + 1 < s_end) push(++irow);
-        else pending = true;  // taken from the counter at the next issue (after the barrier)
-#else
         ++irow;
-#endif
       }
     };
     auto dma_unit = [&](const LK_GLOBAL uint8_t *base, int ubytes, int sl) {
@@ -597,34 +512,12 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 #pragma unroll
       for (int j = 0; j < G::L; j++) {
         int off = j * 1024 + lane * 16;
-        if (LK_TIGHT_SLOTS) {  // lanes past the unit stay idle (their LDS bytes belong to the next slot)
-          if (off < ubytes)
-            __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + off), (LK_LDS void *)(slot + j * 1024), 16, 0,
-                                             LK_WEIGHT_AUX);
-          continue;
-        }
         off = off < ubytes ? off : 0;  // lanes past the unit re-read its first 16 B (never decoded)
         __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + off), (LK_LDS void *)(slot + j * 1024), 16, 0,
-                                         LK_WEIGHT_AUX);
+                                         2);
       }
     };
     auto issue = [&]() {
-#if LK_STREAM_DYN
-      if (pending) {
-        // by asm: the compiler would drain every LDS-DMA in flight (vmcnt(0)) before an LDS
-        // atomic it cannot tell apart from the ring slots
-        unsigned v = 0;
-        if (lane == 0)
-          asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
-                       : "=v"(v) : "v"((uint32_t)(uintptr_t)rctr), "v"((unsigned)CR) : "memory");
-        const int r = (int)__builtin_amdgcn_readfirstlane(v);
-        if (r >= R) { exhausted = true; return; }
-        pending = false;
-        irow = r;
-        s_end = min(r + CR, R);
-        push(r);
-      }
-#endif
       dma_unit(A + (int64_t)irow * RB + (int64_t)ich * G::UB, (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB), islot);
       advance();
       islot = (islot + 1 == G::D) ? 0 : islot + 1;
@@ -667,10 +560,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         x_store(r, xv);
       }
     };
-    auto weight_prologue = [&](bool with_x) __attribute__((always_inline)) {
+    auto weight_prologue = [&]() __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < G::D; k++) {
-        if (with_x && LK_PROLOGUE_ORDER == 1 && k == 1) dma_x();
         const bool real = k < nunits;
         const LK_GLOBAL uint8_t *base = real ? A + (int64_t)irow * RB + (int64_t)ich * G::UB : (const LK_GLOBAL uint8_t *)a_node;
         const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : (int)min((int64_t)G::UB, RB);
@@ -691,7 +583,6 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       //    one 128-B line each); the shard's last arriver arrives on the top word
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      init_ctr();  // published by the barriers below, before any wave takes a row from it
       unsigned *bsync = sync + (bar - 1) * kChainLine * 9;
       if (wave == 0 && lane == 0) {
         const int sh = (int)blockIdx.x % 8;
@@ -700,10 +591,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         if (prev == shn - 1) __hip_atomic_fetch_add(bsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       // 2. the weights do not depend on the previous stage: their stream starts now
-      weight_prologue(false);
+      weight_prologue();
       // 3. one lane waits until all 8 shards are complete (bounded: a grid that is not
       //    co-resident sets the timeout flag and runs on instead of hanging)
-#ifndef LK_CHAIN_NOWAIT  // lab skeleton (wrong results): the stages run on without waiting
       if (wave == 0 && lane == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), bound = lk_sync_wait_bound;
         const unsigned nsh = gridDim.x < 8 ? gridDim.x : 8;
@@ -716,7 +606,6 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
           __builtin_amdgcn_s_sleep(2);
         }
       }
-#endif
       asm volatile("" ::: "memory");  // the loads below stay after the poll
       __builtin_amdgcn_s_barrier();
       // 4. the stage's activations (sc1 loads: the youngest, so wait for all)
@@ -725,11 +614,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       __builtin_amdgcn_s_barrier();
     } else if (sync) {  // chain plans, a later segment of a stage (or stage 0): no grid barrier
       if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
-      init_ctr();
       {  // the first round of activation loads ahead of the weight prologue, waited for alone
         f32x4 xv[4];
         x_issue(0, xv);
-        weight_prologue(false);
+        weight_prologue();
         wait_vmcnt<G::D * G::L>();
         x_store(0, xv);
       }
@@ -743,20 +631,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       __builtin_amdgcn_s_barrier();
     } else {
     if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
-    init_ctr();
-    if (LK_PROLOGUE_ORDER == 0 || LK_PROLOGUE_ORDER == 2) dma_x();
-    if (LK_PROLOGUE_ORDER == 2) {  // the image first, alone: its latency is not queued behind the weight burst
-      wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-    }
-    weight_prologue(true);
-
-    if (LK_PROLOGUE_ORDER != 2) {
-#ifndef LK_NO_XWAIT  // lab: decode against whatever the image holds (wrong results): the x latency's share
-      wait_vmcnt<(LK_PROLOGUE_ORDER == 0 ? G::D : G::D - 1) * G::L>();  // this wave's activation DMA has landed
-      __builtin_amdgcn_s_barrier();  // ... and every other wave's
-#endif
-    }
+    dma_x();
+    weight_prologue();
+    wait_vmcnt<G::D * G::L>();     // this wave's activation DMA has landed
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
     }
 
     // 2. activations into VGPRs in decode order, and Σx per block
@@ -801,24 +679,14 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       }
     }
 
-    if (si == 0) LK_TRACE(1);
     int slot = 0, u = 0;
     LK_GLOBAL float *out = (LK_GLOBAL float *)dst_node + (int64_t)r0 * dst_stride;
-#if LK_STREAM_DYN
-    // more_units: another unit may be issued; full_ring: D − 1 units were issued past unit u
-#define LK_MORE_UNITS (!exhausted)
-#define LK_FULL_RING (issued >= u + G::D)
-    for (int dq = 0; dq < qn; dq++) {  // qn grows as the issue side takes rows
-#else
-#define LK_MORE_UNITS (issued < nunits)
-#define LK_FULL_RING (u + G::D - 1 < nunits)
     for (int row = 0; row < nrows; row++) {
-#endif
       float acc = 0.f;
 #pragma unroll
       for (int c = 0; c < CPL; c++) {
         if (c < nch) {
-          if (LK_FULL_RING) wait_vmcnt<G::VMCNT>();
+          if (u + G::D - 1 < nunits) wait_vmcnt<G::VMCNT>();  // a full ring: D − 1 units issued past unit u
           else wait_vmcnt<0>();
           const uint32_t *rp = (const uint32_t *)(ring + slot * G::SLOT + lane * G::PB);
           uint32_t w[G::PDW];
@@ -839,49 +707,25 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
 #pragma unroll
             for (int k = 0; k < G::PDW; k++) w[k] = rp[k];
           }
-#if LK_EARLY_ISSUE  // lab: refill the slot before the decode instead of after it
-          if (LK_MORE_UNITS) {
+          if (issued < nunits) {
             wait_lgkmcnt0();
             issue();
           }
-#endif
-#ifdef LK_NO_DECODE  // lab: the decode removed (wrong results): the DMA + LDS-read skeleton alone
-          const float v = __builtin_bit_cast(float, w[0] ^ w[G::PDW - 1]);
-#else
           float v;
           if constexpr (QT == LK_TYPE_Q4_K) v = q4k_stream_dot(kh, kc0, kc1, lane, xr[c], xs0[c], xs1[c], q63);
           else if constexpr (QT == LK_TYPE_Q2_K) v = q2k_stream_dot(q2s, q2c, q2d, xr[c], xq[c], q63);
           else v = pair_dot_s<QT>(w, xr[c], xs0[c], xs1[c]);
-#endif
           acc += valid[c] ? v : 0.f;
-#if !LK_EARLY_ISSUE
-          if (LK_MORE_UNITS) {
-            wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
-            issue();
-          }
-#endif
           slot = (slot + 1 == G::D) ? 0 : slot + 1;
           ++u;
         }
       }
-#if LK_STREAM_DYN
-      if (si == 0 && dq == 0) LK_TRACE(2);
-      const int row = __builtin_amdgcn_readfirstlane(rowq[dq & 7]);
-#else
-      if (si == 0 && row == 0) LK_TRACE(2);
-#endif
-#ifdef LK_NO_REDUCE  // lab: the per-row reduction removed (wrong results)
-      const float tot = acc;
-#else
       const float tot = dpp_sum(acc);
-#endif
       if (lane == 63) {
         if (sync) __hip_atomic_store(out + (int64_t)row * dst_stride, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
         else out[(int64_t)row * dst_stride] = tot;
       }
     }
-#undef LK_MORE_UNITS
-#undef LK_FULL_RING
   }
   if (sync) {
     // chain plans: the workgroup that leaves last (every workgroup has passed every barrier)
@@ -896,7 +740,6 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
         for (int b = lane; b <= nbar * 9; b += kWave) __hip_atomic_store(sync + b * kChainLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  LK_TRACE(3);
 }
 
 struct GenericArgs {
@@ -945,49 +788,64 @@ struct XSplitArgs {
   int32_t q4_order;   // 1: k order (0,2,4,6,1,3,5,7) within each 8; 2: (0,4,1,5,2,6,3,7) (lk_skinny.hpp)
 };
 
-// One wave per (x-tile, block).
+// One wave per kXsItems consecutive (x-tile, block) items, every item's loads issued before any is
+// used. One item per wave is the fastest measured (C5 55.6 vs 57.3 us with four: 16 waves per CU
+// in flight beat 4 waves with 32 loads each).
+constexpr int kXsItems = 1;
 __global__ __launch_bounds__(256) void xsplit_kernel(XSplitArgs g) {
   const int lane = threadIdx.x & 63;
-  const int64_t nblk = g.K / 32, ntx = (g.N + 15) / 16;
-  const int64_t idx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (idx >= ntx * nblk) return;
-  const int64_t t = idx / nblk, kb = idx % nblk;
-  const int64_t n = 16 * t + (lane & 15);
-  const int64_t k0 = 32 * kb + 8 * (lane >> 4);
-  float v[8];
-  float part = 0.f;
+  const int64_t nblk = g.K / 32, ntx = (g.N + 15) / 16, total = ntx * nblk;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kXsItems;
+  if (base >= total) return;
+  float v[kXsItems][8];
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
-    const int kk = g.q4_order == 2 ? ((j >> 1) + 4 * (j & 1)) : g.q4_order ? ((j & 3) * 2 + (j >> 2)) : j;
-    v[j] = (n < g.N) ? *(const float *)(g.b + n * g.b_nb0 + (k0 + kk) * g.b_nb1) : 0.f;
-    part += v[j];
-  }
-  uint32_t hi[4], lo[4];
-  float hsum = 0.f;
+  for (int it = 0; it < kXsItems; it++) {
+    const int64_t idx = min(base + it, total - 1);
+    const int64_t t = idx / nblk, kb = idx % nblk;
+    const int64_t n = 16 * t + (lane & 15);
+    const int64_t k0 = 32 * kb + 8 * (lane >> 4);
 #pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    uint32_t h[2], l[2];
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const uint32_t bx = __builtin_bit_cast(uint32_t, v[j + q]);
-      const float r = v[j + q] - __builtin_bit_cast(float, bx & 0xFFFF0000u);  // exact
-      uint32_t br = __builtin_bit_cast(uint32_t, r);
-      br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even (r is finite, |r| < 2^-7·|x|)
-      h[q] = bx;
-      l[q] = br;
-      // q4_order 2 (lk_skinny.hpp) cancels a 136-fold offset against this sum: take it over the
-      // split itself, hi + lo, so the split's own error is not amplified
-      if (g.q4_order == 2) hsum += __builtin_bit_cast(float, bx & 0xFFFF0000u) + __builtin_bit_cast(float, br & 0xFFFF0000u);
+    for (int j = 0; j < 8; j++) {
+      const int kk = g.q4_order == 2 ? ((j >> 1) + 4 * (j & 1)) : g.q4_order ? ((j & 3) * 2 + (j >> 2)) : j;
+      v[it][j] = (n < g.N) ? *(const float *)(g.b + n * g.b_nb0 + (k0 + kk) * g.b_nb1) : 0.f;
     }
-    hi[j / 2] = __builtin_amdgcn_perm(h[1], h[0], 0x07060302u);
-    lo[j / 2] = __builtin_amdgcn_perm(l[1], l[0], 0x07060302u);
   }
-  g.frag[(idx * kXSplits + 0) * 64 + lane] = u32x4{hi[0], hi[1], hi[2], hi[3]};
-  g.frag[(idx * kXSplits + 1) * 64 + lane] = u32x4{lo[0], lo[1], lo[2], lo[3]};
-  if (g.q4_order == 2) part = hsum;
-  part += __shfl_xor(part, 16, kWave);
-  part += __shfl_xor(part, 32, kWave);
-  if (lane < 16) g.xsum[kb * (ntx * 16) + n] = g.mult * part;
+#pragma unroll
+  for (int it = 0; it < kXsItems; it++) {
+    const int64_t idx = base + it;
+    if (idx >= total) break;
+    const int64_t t = idx / nblk, kb = idx % nblk;
+    const int64_t n = 16 * t + (lane & 15);
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j++) part += v[it][j];
+    uint32_t hi[4], lo[4];
+    float hsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      uint32_t h[2], l[2];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t bx = __builtin_bit_cast(uint32_t, v[it][j + q]);
+        const float r = v[it][j + q] - __builtin_bit_cast(float, bx & 0xFFFF0000u);  // exact
+        uint32_t br = __builtin_bit_cast(uint32_t, r);
+        br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even (r is finite, |r| < 2^-7·|x|)
+        h[q] = bx;
+        l[q] = br;
+        // q4_order 2 (codes 128 + n) cancels a 136-fold offset against this sum: take it over the
+        // split itself, hi + lo, so the split's own error is not amplified
+        if (g.q4_order == 2) hsum += __builtin_bit_cast(float, bx & 0xFFFF0000u) + __builtin_bit_cast(float, br & 0xFFFF0000u);
+      }
+      hi[j / 2] = __builtin_amdgcn_perm(h[1], h[0], 0x07060302u);
+      lo[j / 2] = __builtin_amdgcn_perm(l[1], l[0], 0x07060302u);
+    }
+    g.frag[(idx * kXSplits + 0) * 64 + lane] = u32x4{hi[0], hi[1], hi[2], hi[3]};
+    g.frag[(idx * kXSplits + 1) * 64 + lane] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+    if (g.q4_order == 2) part = hsum;
+    part += __shfl_xor(part, 16, kWave);
+    part += __shfl_xor(part, 32, kWave);
+    if (lane < 16) g.xsum[kb * (ntx * 16) + n] = g.mult * part;
+  }
 }
 
 // bf16 codes 128 + n of the 8 nibbles of dword u, slots in k order (0,4,1,5,2,6,3,7).
@@ -1339,7 +1197,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_q_lds_kernel(GemmArgs g) {
     uint8_t *slot = smem + sl * G::STAGE;
 #pragma unroll
     for (int c = 0; c < G::C; c++) {
-      if (c < G::CA) dma16<LK_WEIGHT_AUX == 2>(base_a, vofs[c], slot + ldso[c]);
+      if (c < G::CA) dma16<2 == 2>(base_a, vofs[c], slot + ldso[c]);
       else if (c < G::CA + G::CX) dma16<false>(base_x, vofs[c], slot + ldso[c]);
       else dma16<false>(base_t, vofs[c], slot + ldso[c]);
     }
@@ -1425,9 +1283,6 @@ __global__ __launch_bounds__(NW * 64) void gemm_q_lds_kernel(GemmArgs g) {
 
 // Weight DMA policy of the skinny GEMM: default (0) keeps lines in L2, where the neighbouring
 // slice's workgroup (same XCD) reads the 128-B line its piece shares with this one.
-#ifndef LK_SKINNY_NT
-#define LK_SKINNY_NT 0
-#endif
 
 template <int QT, int NT> struct SkinnyGeom {
   static constexpr int NW = 4;                         // waves per workgroup: one per SIMD
@@ -1652,9 +1507,6 @@ __device__ __forceinline__ void store_partial(bool fused, const __amdgpu_buffer_
   else *(f32x4 *)(partial + idx) = v;
 }
 
-#ifdef LK_SKINNY_TRACE
-__device__ uint64_t *lk_strace_buf;
-#endif
 
 template <int QT, int NT>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
@@ -1667,18 +1519,6 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t *ring = smem + G::XB + G::TB + wave * D * G::SLOT;
-#ifdef LK_SKINNY_TRACE
-  // the buffer pointer is read once, by a scalar load (a vector load would wait behind the DMA)
-  uint64_t *const strace = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_strace_buf)[0];
-#define LK_STRACE(slot_)                                                                                     \
-  do {                                                                                                      \
-    if (lane == 0 && strace)                                                                                \
-      strace[((size_t)blockIdx.x * NW + wave) * 8 + (slot_)] = __builtin_amdgcn_s_memrealtime();             \
-  } while (0)
-#else
-#define LK_STRACE(slot_) do {} while (0)
-#endif
-  LK_STRACE(0);
   // XCD-aware task order (speed only: dispatch is observed round-robin over the 8 XCDs):
   // workgroup b runs task (b % 8)·(grid / 8) + b / 8, so the slices of one row range — which
   // share the 128-B lines at their boundaries — and a range's neighbours land on one L2.
@@ -1712,7 +1552,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
 #pragma unroll
     for (int j = 0; j < L; j++) {
       const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
-      dma16<LK_SKINNY_NT>(tb, vofs, ring + sl * G::SLOT + j * 1024);
+      dma16<0>(tb, vofs, ring + sl * G::SLOT + j * 1024);
     }
   };
   // 1. the HBM stream starts with one unit per wave
@@ -1765,12 +1605,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
       if (lane < 16) tlds[f * 16 + lane] = part;
     }
   }
-  LK_STRACE(1);
   // 3. the rest of the ring
   for (int u = 1; u < min(D, nunits); u++) issue(u, u);
   wait_lgkmcnt0();
   __builtin_amdgcn_s_barrier();
-  LK_STRACE(2);
   // 4. every wave holds all of the slice's activation fragments
   u32x4 xh[16][NT], xl[16][NT];
 #pragma unroll
@@ -1793,7 +1631,6 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
     if (u + D - 1 < nunits) wait_vmcnt_prog<(D - 1) * L, NT, D>(u);
     else wait_vmcnt<0>();
     asm volatile("" ::: "memory");  // the slot's LDS reads stay behind the wait
-    if (u == 0) LK_STRACE(3);
     f32x4 acc[NT];
 #pragma unroll
     for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1806,7 +1643,6 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
     }
     if (nb == SB) skinny_blocks<QT, NT, SB, G::WPB, true, 0>(wd, tlds, nb, lane, xh, xl, acc);
     else skinny_blocks<QT, NT, SB, G::WPB, false, 0>(wd, tlds, nb, lane, xh, xl, acc);
-    if (u == 0) LK_STRACE(7);
     wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
     if (u + D < nunits) issue(u + D, slot);
     slot = (slot + 1 == D) ? 0 : slot + 1;
@@ -1825,12 +1661,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
           if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
       }
     }
-    if (u == 0) LK_STRACE(4);
   }
-  LK_STRACE(5);
   wait_vmcnt<0>();
-  LK_STRACE(6);
-#undef LK_STRACE
   if (g.rsync)
     splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
                             g.d_nb0, g.d_nb1, wave, lane);
@@ -1878,29 +1710,14 @@ template <int J> __device__ __forceinline__ void wait_vmcnt_rt(int x) {
   else wait_vmcnt_rt<J - 1>(x);
 }
 
-// Block B (0..7) of this wave's half: x held as [8][NT]; T (Q4_1) indexed by the slice block.
-// Lab skeletons (LK_SKP_SKEL, wrong results; tools/lab/skp_skel.sh): 1 no MFMAs, 2 no decode,
-// 3 no ring refills, 4 no accumulator hand-off, 5 no decode / MFMA / scale.
-#ifndef LK_SKP_SKEL
-#define LK_SKP_SKEL 0
-#endif
+// Block B (0..7) of this wave's half: x held as [8][NT]; T (Q4_0 / Q4_1) indexed by the slice block.
 template <int QT, int NT, int B, int WPB>
 __device__ __forceinline__ void skinny_pair_block(const uint32_t (&w)[WPB], const float *tl, int lane, const u32x4 (&xh)[8][NT],
                                                   const u32x4 (&xl)[8][NT], f32x4 (&acc)[NT]) {
   constexpr int OB = B * QTraits<QT>::BB;
   bf16x8 wf;
   float s1, s2 = 0.f;
-#if LK_SKP_SKEL == 5
-  acc[0].x += __builtin_bit_cast(float, w[0] & 0x3FFFFFFFu);
-  return;
-#endif
-#if LK_SKP_SKEL == 2
-  wf = __builtin_bit_cast(bf16x8, u32x4{w[WPB - 1], w[WPB - 1] ^ 1u, w[WPB - 1] ^ 2u, w[WPB - 1] ^ 3u});
-  s1 = __builtin_bit_cast(float, w[0] & 0x3FFFFFFFu);
-  if constexpr (false) {
-#else
   if constexpr (QT == LK_TYPE_Q4_1) {
-#endif
     wf = Q4Frag<0>::make(w[1]);
     s1 = 512.f * h2f(w[0]);
     s2 = h2f(w[0] >> 16);
@@ -1925,13 +1742,9 @@ __device__ __forceinline__ void skinny_pair_block(const uint32_t (&w)[WPB], cons
   for (int j = 0; j < NT; j++) {
     f32x4 t = {0.f, 0.f, 0.f, 0.f};
     if constexpr (QT != LK_TYPE_Q8_0) t = *(const f32x4 *)(tl + (B * NT + j) * 16 + (lane >> 4) * 4);
-#if LK_SKP_SKEL == 1
-    f32x4 p = __builtin_bit_cast(f32x4, wf);
-#else
     f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf,
                                                       QT == LK_TYPE_Q4_0 ? t : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
-#endif
     accumulate_s<QT == LK_TYPE_Q4_1>(acc[j], s1, s2, p, t);
   }
 }
@@ -1961,15 +1774,6 @@ __device__ __forceinline__ void lds_st(int *p, int v) {
   asm volatile("" ::: "memory");
 }
 
-#ifndef LK_SKP_EARLY
-#define LK_SKP_EARLY 0
-#endif
-#ifndef LK_SKP_PRIO
-#define LK_SKP_PRIO 0
-#endif
-#ifndef LK_SKP_STAGGER
-#define LK_SKP_STAGGER 0
-#endif
 template <int QT, int NT>
 __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   using G = SkinnyPairGeom<QT, NT>;
@@ -1983,20 +1787,6 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int p = wave & 3, h = wave >> 2;
   uint8_t *ring = smem + G::XB + G::TB + G::EB + G::FB + wave * D * G::SLOT;
-#ifdef LK_SKINNY_TRACE  // tools/lab/skinny_trace.hip (PAIR=1): the same stamps as gemm_skinny_kernel
-  uint64_t *const strace = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_strace_buf)[0];
-#define LK_PTRACE(slot_)                                                                                     \
-  do {                                                                                                      \
-    if (lane == 0 && strace)                                                                                \
-      strace[((size_t)blockIdx.x * NW + wave) * 16 + (slot_)] = __builtin_amdgcn_s_memrealtime();            \
-  } while (0)
-#define LK_PNOW() __builtin_amdgcn_s_memtime()
-  uint64_t c_dma = 0, c_comp = 0, c_issue = 0, c_hand = 0, c_store = 0;  // shader cycles per phase
-#else
-#define LK_PTRACE(slot_) do {} while (0)
-#define LK_PNOW() 0ull
-#endif
-  LK_PTRACE(0);
   // XCD-aware task order, as gemm_skinny_kernel
   const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
   if (task >= g.tasks) return;  // grid padding (before any barrier: the whole workgroup leaves)
@@ -2030,15 +1820,12 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
 #pragma unroll
     for (int j = 0; j < L; j++) {
       const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
-      dma16<LK_SKINNY_NT>(tb, vofs, ring + sl * G::SLOT + j * 1024);
+      dma16<0>(tb, vofs, ring + sl * G::SLOT + j * 1024);
     }
   };
 
-  // 0. (lab, LK_SKP_EARLY=1) the weight ring first, so its HBM round trip overlaps the
-  //    activation loads (their compiler waits then also wait for these older DMAs): measured
-  //    slower on C3, 24.0 vs 23.1 us per call (the activation loads queue behind the burst)
-  if (LK_SKP_EARLY && myL)
-    for (int u = 0; u < min(D, nunits); u++) issue(u, u);
+  // (the weight ring issued before the activation loads measured slower on C3, 24.0 vs 23.1 us
+  // per call: the activation loads queue behind the burst)
   // 1. activations of the slice -> LDS fragments, as gemm_skinny_kernel (compiler-visible loads:
   //    issued before the weight ring, so waiting for them never waits for it)
   float v[G::FPW][8];
@@ -2090,9 +1877,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       if (lane < 16) tlds[f * 16 + lane] = QT == LK_TYPE_Q4_0 ? -136.f * part : part;
     }
   }
-  LK_PTRACE(1);
-  // 2. the weight ring, after the split (LK_SKP_EARLY=0, the default)
-  if (!LK_SKP_EARLY && myL)
+  // 2. the weight ring, after the split (0=0, the default)
+  if (!0 && myL)
     for (int u = 0; u < min(D, nunits); u++) issue(u, u);
   wait_lgkmcnt0();
   __builtin_amdgcn_s_barrier();  // fragments and flags visible (bare: the ring stays in flight)
@@ -2108,27 +1894,12 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       xl[b][j] = xf[64];
     }
   const float *tl = tlds + 8 * h * NT * 16;
-  LK_PTRACE(2);
-  // lab: LK_SKP_PRIO 1 raises the h = 1 wave's issue priority, 2 the h = 0 wave's; LK_SKP_STAGGER
-  // delays the h = 0 wave's first unit (s_sleep units of 64 cycles) so the pair's MFMA phases
-  // interleave instead of contending for the SIMD's one MFMA pipe
-#if LK_SKP_PRIO == 1
-  if (h == 1) __builtin_amdgcn_s_setprio(1);
-#elif LK_SKP_PRIO == 2
-  if (h == 0) __builtin_amdgcn_s_setprio(1);
-#endif
-#if LK_SKP_STAGGER
-  if (h == 0) for (int i = 0; i < LK_SKP_STAGGER; i++) __builtin_amdgcn_s_sleep(1);
-#endif
 
   const int N16 = 16 * NT;
   // the partial slabs as a buffer (fused reduction: sc1 stores and loads; the host checks the size)
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
   const int SH = h == 0 ? NT : 0;  // stores per unit (at least; slices == 1 may store more)
-#ifdef LK_SKP_STALE
-  uint32_t wd0[8][G::WPB] = {};
-#endif
   for (int u = 0; u < nunits; u++) {
     const int slot = u % D;
     f32x4 acc[NT];
@@ -2136,62 +1907,33 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (myL) {
       // ops younger than this unit's DMA: its successors already issued, and the stores since
-      [[maybe_unused]] const uint64_t q0 = LK_PNOW();
       wait_vmcnt_rt<G::MAXW>(myL * min(D - 1, nunits - 1 - u) + min(u, D) * SH);
       asm volatile("" ::: "memory");
-      [[maybe_unused]] const uint64_t q1 = LK_PNOW();
-      if (u == 0) LK_PTRACE(3);
       uint32_t wd[8][G::WPB];
       {
         const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::RPH;
         const uint8_t *bg = bm + (QT == LK_TYPE_Q8_0 ? 8 : 4) * (lane >> 4);
-#ifdef LK_SKP_STALE  // lab skeleton (wrong results): the weight dwords of the first unit only
-        if (u == 0) skinny_read_all<QT, 8, G::WPB, 0>(bm, bg, wd0);
-#pragma unroll
-        for (int b = 0; b < 8; b++)
-#pragma unroll
-          for (int q = 0; q < G::WPB; q++) wd[b][q] = wd0[b][q] + (uint32_t)u;
-#else
         skinny_read_all<QT, 8, G::WPB, 0>(bm, bg, wd);
-#endif
         asm volatile("" ::: "memory");
       }
       if (nbh == 8) skinny_pair_blocks<QT, NT, G::WPB, true, 0>(wd, tl, nbh, lane, xh, xl, acc);
       else skinny_pair_blocks<QT, NT, G::WPB, false, 0>(wd, tl, nbh, lane, xh, xl, acc);
       wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
-      [[maybe_unused]] const uint64_t q2 = LK_PNOW();
-      if (u + D < nunits && LK_SKP_SKEL != 3) issue(u + D, slot);
-      if (u == 0) LK_PTRACE(7);
-#ifdef LK_SKINNY_TRACE
-      const uint64_t q3 = LK_PNOW();
-      c_dma += q1 - q0; c_comp += q2 - q1; c_issue += q3 - q2;
-#endif
+      if (u + D < nunits) issue(u + D, slot);
     }
     f32x4 *xb = xch + ((u & 1) * 4 + p) * NT * 64 + lane;
     if (h == 1) {
-      if (LK_SKP_SKEL == 4) continue;
-      [[maybe_unused]] const uint64_t h0 = LK_PNOW();
       // the partner has consumed unit u − 2 (this parity's previous contents)
       while (lds_ld(flags + 8 + p) < u - 1) __builtin_amdgcn_s_sleep(1);
-#ifdef LK_SKINNY_TRACE
-      c_hand += LK_PNOW() - h0;
-#endif
 #pragma unroll
       for (int j = 0; j < NT; j++) xb[j * 64] = acc[j];
       lds_st(flags + 2 * p + (u & 1), u + 1);
     } else {
-      if (LK_SKP_SKEL != 4) {
-        [[maybe_unused]] const uint64_t h0 = LK_PNOW();
-        while (lds_ld(flags + 2 * p + (u & 1)) != u + 1) __builtin_amdgcn_s_sleep(1);
-#ifdef LK_SKINNY_TRACE
-        c_hand += LK_PNOW() - h0;
-#endif
+      while (lds_ld(flags + 2 * p + (u & 1)) != u + 1) __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-        for (int j = 0; j < NT; j++) acc[j] += xb[j * 64];
-      }
+      for (int j = 0; j < NT; j++) acc[j] += xb[j * 64];
       lds_st(flags + 8 + p, u + 1);
       // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
-      [[maybe_unused]] const uint64_t s0 = LK_PNOW();
       const int t = t0 + p + u * 4;
       const int64_t m = (int64_t)t * 16 + (lane & 15);
 #pragma unroll
@@ -2206,23 +1948,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
             if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
         }
       }
-#ifdef LK_SKINNY_TRACE
-      c_store += LK_PNOW() - s0;
-#endif
     }
-    if (u == 0) LK_PTRACE(4);
   }
-  LK_PTRACE(5);
   wait_vmcnt<0>();
-  LK_PTRACE(6);
-#ifdef LK_SKINNY_TRACE  // per-phase shader cycles in slots 8..12
-  if (lane == 0 && strace) {
-    uint64_t *q = strace + ((size_t)blockIdx.x * NW + wave) * 16;
-    q[8] = c_dma; q[9] = c_comp; q[10] = c_issue; q[11] = c_hand; q[12] = c_store;
-  }
-#endif
-#undef LK_PTRACE
-#undef LK_PNOW
   if (g.rsync)
     splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
                             g.d_nb0, g.d_nb1, wave, lane);
@@ -2272,11 +2000,7 @@ template <int QT> struct WideGeom {
   static constexpr int T_OFF = W_BYTES + X_BYTES, DUMMY = T_OFF + (T_INST ? 1024 : 0);
   static constexpr bool NEED_DUMMY = WX && !T_SPARE;
   static constexpr int STAGE = DUMMY + (NEED_DUMMY ? 1024 : 0);
-#ifdef LK_WIDE_D
-  static constexpr int D = LK_WIDE_D;
-#else
   static constexpr int D = (kLdsBytes / STAGE) > 3 ? 3 : (kLdsBytes / STAGE);
-#endif
   static constexpr int LDS = D * STAGE;
   static constexpr int OVERREAD = WIN - SB * BB;                // bytes read past a row's last block
   static_assert(D >= 2, "ring");
@@ -2398,7 +2122,9 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
       // this K-group's blocks of the stage into registers with one burst of LDS reads, so the
       // slot can be refilled at once and the MFMAs never wait on LDS
       constexpr int WD = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
-      constexpr bool EARLY = QT == LK_TYPE_Q8_0;  // Q4_0 / Q4_1 read their Σx during the compute
+      // Q4_0 / Q4_1 read their Σx during the compute (an early refill with T in a ring of its own, or
+      // one barrier per stage refilling the previous stage's slot, measured no faster on C5)
+      constexpr bool EARLY = !G::T_INST;
       uint32_t wd[BPG][MT][WD];
       u32x4 xh[BPG][NT], xl[BPG][NT];
 #pragma unroll

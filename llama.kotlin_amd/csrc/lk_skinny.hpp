@@ -30,11 +30,6 @@
 
 namespace lk {
 
-// Lab knobs (compile time): LK_SK_PRIO raises the h = 1 wave's issue priority (it is the younger
-// wave of its SIMD and otherwise loses VALU arbitration, while its partner waits in the hand-off).
-#ifndef LK_SK_PRIO
-#define LK_SK_PRIO 1
-#endif
 
 // Bytes per 32 weights: Q4_0 18, Q4_1 20, and Q4_K 18 (a 144-byte block of 256 weights: d, dmin,
 // 12 scale bytes, 128 code bytes; core/GGMLComputeOps.kt:241-310). For Q4_K a "block" here is
@@ -193,20 +188,15 @@ __device__ __forceinline__ void sk_scale(const f32x4 (&p)[NT], float s1, int nb,
 
 // Scheduling hint for a unit's block section (one basic block): alternate each MFMA with a few
 // VALU instructions, so the decode of the next block and the scaling of the previous one issue in
-// the MFMA gaps instead of as one VALU run ahead of a dependent MFMA chain. LK_SK_SCHED = VALU per
+// the MFMA gaps instead of as one VALU run ahead of a dependent MFMA chain. 3 = VALU per
 // MFMA (0: leave it to the compiler).
-#ifndef LK_SK_SCHED
-#define LK_SK_SCHED 3
-#endif
 template <int NMFMA>
 __device__ __forceinline__ void sk_interleave() {
-#if LK_SK_SCHED > 0
 #pragma unroll
   for (int i = 0; i < NMFMA; i++) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // one MFMA
-    __builtin_amdgcn_sched_group_barrier(0x002, LK_SK_SCHED, 0);   // then VALU
+    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // then VALU
   }
-#endif
 }
 
 // All NBW blocks of a unit, pipelined: block B's MFMAs go out before block B − 1 is scaled in.
@@ -222,22 +212,6 @@ __device__ __forceinline__ void sk_blocks(const uint32_t (&w)[NBW][WPB], const u
     else sk_blocks<QT, NT, WPB, MASK, B + 1, NBW>(w, xh, xl, nb, p, s1, acc, hd);
   }
 }
-
-// Lab timeline (tools/lab/sk_trace.hip defines LK_SK_TRACE): per wave, s_memrealtime at entry,
-// after the barrier, unit 0 landed / computed, loop done; s_memtime cycles summed over the units
-// waiting for the DMA, computing, and in the hand-off.
-#ifdef LK_SK_TRACE
-__device__ uint64_t *lk_sktrace_buf;
-#define LK_SKT_NOW() __builtin_amdgcn_s_memtime()
-#define LK_SKT(slot_, v_)                                                                                  \
-  do {                                                                                                     \
-    uint64_t *tb_ = (uint64_t *)((const __attribute__((address_space(4))) uint64_t *)&lk_sktrace_buf)[0];   \
-    if (lane == 0 && tb_) tb_[((size_t)blockIdx.x * 8 + wave) * 8 + (slot_)] = (v_);                        \
-  } while (0)
-#else
-#define LK_SKT_NOW() 0ull
-#define LK_SKT(slot_, v_) do {} while (0)
-#endif
 
 template <int QT, int NT>
 __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
@@ -289,7 +263,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 #pragma unroll
     for (int j = 0; j < L; j++) {
       const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
-      dma16l<LK_SKINNY_NT>(tb, vofs, ring + sl * G::SLOT + j * 1024);
+      dma16l<0>(tb, vofs, ring + sl * G::SLOT + j * 1024);
     }
   };
 
@@ -400,10 +374,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       const int bl = 4 * c + (lane >> 4);
       sf[c][j] = bl < nbh ? tlds[(G::SBH * h + bl) * 16 * NT + 16 * j + (lane & 15)] : 0.f;
     }
-#if LK_SK_PRIO
   if (h) __builtin_amdgcn_s_setprio(1);
-#endif
-  LK_SKT(1, __builtin_amdgcn_s_memrealtime());
 
   const int N16 = 16 * NT;
   const __amdgpu_buffer_rsrc_t prs =
@@ -412,16 +383,12 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   // priority, is ahead), so neither wave idles while the other computes: the two waves of a SIMD
   // overlap their VALU / MFMA streams.
   auto collect = [&](int v, const f32x4 (&mine)[NT]) __attribute__((always_inline)) {
-    [[maybe_unused]] const uint64_t c2 = LK_SKT_NOW();
     const LK_LDS f32x4 *xb = xch + ((v & 1) * 4 + p) * NT * 64 + lane;
     while (ldsl_ld(flags + 2 * p + (v & 1)) != v + 1) __builtin_amdgcn_s_sleep(1);
     f32x4 sum[NT];
 #pragma unroll
     for (int j = 0; j < NT; j++) sum[j] = mine[j] + xb[j * 64];
     ldsl_st(flags + 8 + p, v + 1);
-#ifdef LK_SK_TRACE
-    c_hand += LK_SKT_NOW() - c2;
-#endif
     // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
     const int t = t0 + p + v * 4;
     const int64_t m = (int64_t)t * 16 + (lane & 15);
@@ -444,17 +411,11 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     f32x4 acc[NT];
 #pragma unroll
     for (int j = 0; j < NT; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    [[maybe_unused]] const uint64_t c0 = LK_SKT_NOW();
     if (myL) {
       // ops younger than this unit's DMA: its successors already issued, and the stores of the
       // collections since (h = 0: NT or more per iteration from iteration 1 on)
       wait_vmcnt_rt<G::MAXW>(myL * min(D - 1, nunits - 1 - u) + (h == 0 ? NT * min(D, max(u - 1, 0)) : 0));
       asm volatile("" ::: "memory");
-#ifdef LK_SK_TRACE
-      const uint64_t c1 = LK_SKT_NOW();
-      c_wait += c1 - c0;
-      if (u == 0) LK_SKT(2, __builtin_amdgcn_s_memrealtime());
-#endif
       uint32_t wd[8][G::WPB];
       uint32_t eb[2];  // the header (d, and m for Q4_1) of block 4c + (lane >> 4) of the lane's row
       uint32_t ek[2];  // Q4_K: sub-block 4c + (lane >> 4)'s min-high byte
@@ -489,16 +450,12 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         hd.dmin = h2f(hd.h[0] >> 16);
       }
       f32x4 pp[NT];
-#ifdef LK_SK_NOCOMP  // lab: the skeleton without decode / MFMAs
-      acc[0].x += __builtin_bit_cast(float, wd[0][0] ^ wd[7][1]);
-#else
       if (nbh == 8) {
         sk_blocks<QT, NT, G::WPB, false, 0, 8>(wd, xh, xl, nbh, pp, 0.f, acc, hd);
         sk_interleave<8 * 2 * NT>();
       } else {
         sk_blocks<QT, NT, G::WPB, true, 0, 8>(wd, xh, xl, nbh, pp, 0.f, acc, hd);
       }
-#endif
       // the offsets: acc += Σ_b e_b·S_b over the 8 blocks (f32 MFMA, K = 4 blocks each)
 #pragma unroll
       for (int c = 0; c < 2; c++) {
@@ -517,27 +474,15 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         for (int j = 0; j < NT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(sf[c][j], e, acc[j], 0, 0, 0);
       }
       wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
-#ifdef LK_SK_TRACE
-      const uint64_t c3 = LK_SKT_NOW();
-#endif
       if (u + D < nunits) issue(u + D, slot);
-#ifdef LK_SK_TRACE
-      c_issue += LK_SKT_NOW() - c3;
-      c_comp += LK_SKT_NOW() - c1;
-      if (u == 0) LK_SKT(3, __builtin_amdgcn_s_memrealtime());
-#endif
     }
     if (h == 1) {
-      [[maybe_unused]] const uint64_t c2 = LK_SKT_NOW();
       // the partner has consumed unit u − 2 (this parity's previous contents)
       LK_LDS f32x4 *xb = xch + ((u & 1) * 4 + p) * NT * 64 + lane;
       while (ldsl_ld(flags + 8 + p) < u - 1) __builtin_amdgcn_s_sleep(1);
 #pragma unroll
       for (int j = 0; j < NT; j++) xb[j * 64] = acc[j];
       ldsl_st(flags + 2 * p + (u & 1), u + 1);
-#ifdef LK_SK_TRACE
-      c_hand += LK_SKT_NOW() - c2;
-#endif
     } else {
       if (u > 0) collect(u - 1, prev);
 #pragma unroll
@@ -545,18 +490,11 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     }
   }
   if (h == 0 && nunits > 0) collect(nunits - 1, prev);
-  LK_SKT(0, c_issue);
-  LK_SKT(4, __builtin_amdgcn_s_memrealtime());
-  LK_SKT(5, c_wait);
-  LK_SKT(6, c_comp);
-  LK_SKT(7, c_hand);
   wait_vmcnt<0>();
   if (g.rsync)
     splitk_fused_reduce<G::NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
                                g.d_nb0, g.d_nb1, wave, lane);
 }
 
-#undef LK_SKT
-#undef LK_SKT_NOW
 
 }  // namespace lk
