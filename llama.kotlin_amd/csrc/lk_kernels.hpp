@@ -498,8 +498,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     //      (XOR swizzle: each DMA instruction reads 1 KB of x contiguously, and the per-lane
     //      reads below hit 64 distinct banks); image float4 i = 64·k + lane comes from DMA
     //      instruction k, issued by wave k % 8.
-    //    0 1 issues weight unit 0 first, then the image, then units 1..D-1:
-    //    the HBM stream starts at once and the wait for the image covers unit 0 too.
+    //    The image is issued first, then the weight units (other orders measured no faster:
+    //    DESIGN.md §3.1).
     int irow = 0, ich = 0, islot = 0, issued = 0;
     auto advance = [&]() __attribute__((always_inline)) {  // past an issued unit
       if (++ich == nch) {
@@ -1877,8 +1877,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       if (lane < 16) tlds[f * 16 + lane] = QT == LK_TYPE_Q4_0 ? -136.f * part : part;
     }
   }
-  // 2. the weight ring, after the split (0=0, the default)
-  if (!0 && myL)
+  // 2. the weight ring, after the split
+  if (myL)
     for (int u = 0; u < min(D, nunits); u++) issue(u, u);
   wait_lgkmcnt0();
   __builtin_amdgcn_s_barrier();  // fragments and flags visible (bare: the ring stays in flight)
