@@ -303,25 +303,32 @@ def roofline(torch, plans, local_by_layer, stream, world, reps=10):
     avg_s = e0.elapsed_time(e1) / 1e3 / n
     nbytes = sum(a.ne[1] * a.ne[0] // 32 * Q4_0_BLOCK + 4 * a.ne[0] + 4 * a.ne[1] for (a, _, _) in local_by_layer[0])
     achieved = nbytes / avg_s / 1e9
-    # the committed PMC profile is of the N = 1 layer launch; a row shard is a different launch
-    traffic, src = pmc_traffic("gemv_stream_kernel<2, 3>") if world == 1 else (None, None)
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-            "kernel": "gemv_stream_kernel<Q4_0,3> (the 7 matrices of one layer in one launch)",
-            "bytes_per_launch": nbytes, "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": n,
-            "hip_graph": g is not None}
+    # the committed profile is of the N = 1 layer launch; a row shard is a different launch
+    prof, src = pmc_traffic("gemv_stream_kernel<2, 3>") if world == 1 else (None, None)
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": prof["hbm_bytes_per_launch"] if prof else None,
+           "traffic_source": src,
+           "kernel": "gemv_stream_kernel<Q4_0,3> (the 7 matrices of one layer in one launch)",
+           "bytes_per_launch": nbytes, "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": n,
+           "hip_graph": g is not None}
+    if prof and prof.get("mean_us"):
+        # beside the event figure: the same launch's mean kernel duration in the committed rocprof
+        # kernel trace (a profiled run: lower clock, no inter-launch gaps)
+        out["rocprof_mean_us"] = prof["mean_us"]
+        out["rocprof_frac"] = round(nbytes / (prof["mean_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    return out
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC profile of this bench
-    (profiles/rNN/traffic.json: FETCH_SIZE x 2 + WRITE_SIZE per launch, separate --pmc passes of
-    tools/profile.sh, summarised by tools/prof_summary.py); (None, None) when absent."""
+    """The newest committed profile of `kernel` in this bench (profiles/rNN/traffic.json, written
+    by tools/prof_summary.py from tools/profile.sh's runs): HBM bytes per launch (FETCH_SIZE x 2 +
+    WRITE_SIZE, separate --pmc passes) and the kernel trace's mean duration; (None, None) when absent."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
         with open(f) as fh:
             t = json.load(fh)
         if kernel in t.get("kernel", ""):
-            return t["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+            return t, os.path.relpath(f, ROOT)
     return None, None
 
 

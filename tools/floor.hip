@@ -8,6 +8,9 @@
 #define LK_GLOBAL __attribute__((address_space(1)))
 #define LK_LDS __attribute__((address_space(3)))
 
+// per (workgroup, wave): entry, first weight piece landed, exit (s_memrealtime, 100 MHz)
+__device__ uint64_t floor_st[1024 * 8 * 4];
+
 __global__ __launch_bounds__(512) void empty_kernel(float *out) {
   if (out && threadIdx.x == 0 && blockIdx.x == 0) out[0] = 1.f;
 }
@@ -19,6 +22,8 @@ __global__ __launch_bounds__(512) void read_kernel(const uint8_t *src, int64_t b
                                                    float *out) {
   extern __shared__ uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_first = 0;
   const int64_t per = (bytes / gridDim.x) & ~(int64_t)1023;
   const LK_GLOBAL uint8_t *base = (const LK_GLOBAL uint8_t *)src + per * blockIdx.x;
   const int64_t npieces = per / 1024;
@@ -32,13 +37,23 @@ __global__ __launch_bounds__(512) void read_kernel(const uint8_t *src, int64_t b
                                      (LK_LDS void *)(lds + (wave * DEPTH + slot) * 1024), 16, 0, 2);
     slot = slot + 1 == DEPTH ? 0 : slot + 1;
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DEPTH - 1) : "memory");
+    if (!t_first && p >= wave + 8 * (DEPTH - 1)) t_first = __builtin_amdgcn_s_memrealtime();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!t_first) t_first = __builtin_amdgcn_s_memrealtime();
+  const uint64_t t_exit = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && blockIdx.x < 1024) {
+    uint64_t *st = floor_st + ((size_t)blockIdx.x * 8 + wave) * 4;
+    st[0] = t_entry; st[1] = t_first; st[2] = t_exit;
+  }
   __syncthreads();
   if (threadIdx.x == 0) out[blockIdx.x] = *(const float *)(lds);
 }
 
 extern "C" {
+int floor_stamps(uint64_t *host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(floor_st), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
 int floor_empty(int grid, int lds, float *out, void *stream) {
   hipLaunchKernelGGL(empty_kernel, dim3(grid), dim3(512), lds, (hipStream_t)stream, out);
   return (int)hipGetLastError();

@@ -14,11 +14,13 @@ import bench  # noqa: E402
 
 
 def main():
+    import numpy as np
     import torch
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libfloor.so"))
     lib.floor_empty.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.floor_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.floor_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.c_void_p, ctypes.c_void_p]
     s = torch.cuda.Stream(device=dev)
@@ -47,8 +49,18 @@ def main():
                                        ctypes.c_void_p(out.data_ptr()), sp)
                 per, _ = bench._graph_time(torch, run_read, s, 10)
                 us = per / copies * 1e6
-                res[f"read_{name}_d{depth}{'_x' if with_x else ''}"] = {"us": round(us, 3),
-                                                                         "GBps": round(nbytes / us / 1e3, 1)}
+                rec = {"us": round(us, 3), "GBps": round(nbytes / us / 1e3, 1)}
+                if depth == 6 and with_x:  # stamps of the last launch: first piece landed / exit after entry
+                    st = (ctypes.c_uint64 * (1024 * 8 * 4))()
+                    lib.floor_stamps(st, len(st))
+                    a = np.array(list(st), dtype=np.int64).reshape(1024, 8, 4)[:n]
+                    t0 = a[:, :, 0].min()
+                    rel = (a - t0) / 100.0
+                    rec["entry_med"] = round(float(np.median(rel[:, :, 0])), 2)
+                    rec["first_landed_med"] = round(float(np.median(rel[:, :, 1])), 2)
+                    rec["exit_med"] = round(float(np.median(rel[:, :, 2])), 2)
+                    rec["exit_max"] = round(float(rel[:, :, 2].max()), 2)
+                res[f"read_{name}_d{depth}{'_x' if with_x else ''}"] = rec
         del bufs
     print(json.dumps(res), flush=True)
 
