@@ -1738,14 +1738,14 @@ __device__ __forceinline__ void skinny_pair_block(const uint32_t (&w)[WPB], cons
       s1 = h2f(w[0] >> 16);
     }
   }
+  (void)s2;
 #pragma unroll
   for (int j = 0; j < NT; j++) {
-    f32x4 t = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (QT != LK_TYPE_Q8_0) t = *(const f32x4 *)(tl + (B * NT + j) * 16 + (lane >> 4) * 4);
+    // the offset term (Q4_0 −136·Σx, Q4_1 m·Σx) is added once per unit (skinny_pair_offsets)
     f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf,
-                                                      QT == LK_TYPE_Q4_0 ? t : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                                                      f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
-    accumulate_s<QT == LK_TYPE_Q4_1>(acc[j], s1, s2, p, t);
+    accumulate_s<false>(acc[j], s1, 0.f, p, p);
   }
 }
 
@@ -1894,6 +1894,16 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       xl[b][j] = xf[64];
     }
   const float *tl = tlds + 8 * h * NT * 16;
+  // offset operands of v_mfma_f32_16x16x4_f32: lane (n = lane & 15, b' = lane >> 4) holds T of
+  // block 4c + b' of this wave's half and column 16j + n (zero past the wave's blocks)
+  float tf[2][NT];
+#pragma unroll
+  for (int c = 0; c < 2; c++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int bl = 4 * c + (lane >> 4);
+      tf[c][j] = (QT != LK_TYPE_Q8_0 && bl < nbh) ? tl[(bl * NT + j) * 16 + (lane & 15)] : 0.f;
+    }
 
   const int N16 = 16 * NT;
   // the partial slabs as a buffer (fused reduction: sc1 stores and loads; the host checks the size)
@@ -1910,6 +1920,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       wait_vmcnt_rt<G::MAXW>(myL * min(D - 1, nunits - 1 - u) + min(u, D) * SH);
       asm volatile("" ::: "memory");
       uint32_t wd[8][G::WPB];
+      const uint8_t *slot_ptr = ring + slot * G::SLOT;
       {
         const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::RPH;
         const uint8_t *bg = bm + (QT == LK_TYPE_Q8_0 ? 8 : 4) * (lane >> 4);
@@ -1918,6 +1929,20 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       }
       if (nbh == 8) skinny_pair_blocks<QT, NT, G::WPB, true, 0>(wd, tl, nbh, lane, xh, xl, acc);
       else skinny_pair_blocks<QT, NT, G::WPB, false, 0>(wd, tl, nbh, lane, xh, xl, acc);
+      if constexpr (QT != LK_TYPE_Q8_0) {
+        // acc += Σ_b e_b(row)·T_b(column) over the half's 8 blocks, two f32 MFMAs (K = 4 blocks)
+        // per 16-column tile: e = d (Q4_0, T = −136·Σ(hi + lo)) or m (Q4_1, T = Σx); lane
+        // (m = lane & 15, b' = lane >> 4) reads its row's header of block 4c + b'
+        const uint8_t *hrow = slot_ptr + (lane & 15) * G::RPH;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+          const int bl = 4 * c + (lane >> 4);
+          const uint16_t hv = *(const uint16_t *)(hrow + min(bl, 7) * BB + (QT == LK_TYPE_Q4_1 ? 2 : 0));
+          const float e = bl < nbh ? h2f(hv) : 0.f;
+#pragma unroll
+          for (int j = 0; j < NT; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(tf[c][j], e, acc[j], 0, 0, 0);
+        }
+      }
       wait_lgkmcnt0();  // this slot's LDS reads have landed: the DMA may overwrite it
       if (u + D < nunits) issue(u + D, slot);
     }
