@@ -685,16 +685,11 @@ int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   g.dst = (uint8_t *)dst->data + dst->data_offset;
   g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
+  // Q4_0 / Q4_1 at 17 <= N <= 32 on wave pairs (gemm_skinny_pair_kernel), the rest one wave per stream
   const bool one = c.N <= 16;
-  static const int pair = [] { const char *e = getenv("LK_SKINNY_PAIR"); return e ? atoi(e) : 1; }();  // A/B
-  if (pair && (!one || pair == 2)) switch (a->type) {  // LK_SKINNY_PAIR=2: N <= 16 too (lab)
-    case LK_TYPE_Q4_0: return one ? launch_skinny_pair_t<LK_TYPE_Q4_0, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_0, 2>(g, st);
-    case LK_TYPE_Q4_1: return one ? launch_skinny_pair_t<LK_TYPE_Q4_1, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_1, 2>(g, st);
-    default: break;
-  }
   switch (a->type) {
-    case LK_TYPE_Q4_0: return one ? launch_skinny_t<LK_TYPE_Q4_0, 1>(g, st) : launch_skinny_t<LK_TYPE_Q4_0, 2>(g, st);
-    case LK_TYPE_Q4_1: return one ? launch_skinny_t<LK_TYPE_Q4_1, 1>(g, st) : launch_skinny_t<LK_TYPE_Q4_1, 2>(g, st);
+    case LK_TYPE_Q4_0: return one ? launch_skinny_t<LK_TYPE_Q4_0, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_0, 2>(g, st);
+    case LK_TYPE_Q4_1: return one ? launch_skinny_t<LK_TYPE_Q4_1, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_1, 2>(g, st);
     case LK_TYPE_Q8_0: return one ? launch_skinny_t<LK_TYPE_Q8_0, 1>(g, st) : launch_skinny_t<LK_TYPE_Q8_0, 2>(g, st);
     default: return fail(LK_ERR_NOT_IMPLEMENTED, "skinny gemm: type %d", a->type);
   }

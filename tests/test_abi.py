@@ -47,6 +47,31 @@ def test_is_gfx950_code_object(lib):
     assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the embedded offload bundle's target id
 
 
+# Every kernel family the library carries, each reachable by the default dispatch for some shape
+# (DESIGN.md §3); lab variants are built from patched copies of csrc/, never into this library.
+PRODUCT_KERNELS = {
+    "gemv_stream_kernel", "gemv_q_n1_kernel", "gemm_skinny_kernel", "gemm_skinny_pair_kernel",
+    "gemm_sk_kernel", "xsplit_kernel", "gemm_wide_kernel", "splitk_reduce_kernel", "f32_mfma_kernel",
+    "gemm_q_lds_kernel", "gemm_q_mfma_kernel", "kquant_n1_kernel", "kquant_nc_kernel",
+    "kquant_gemv_kernel", "kquant_mul_mat_kernel", "mul_mat_generic_kernel", "dequantize_coop_kernel",
+    "quantize_coop_kernel", "dequantize_kernel", "quantize_kernel", "dot_direct_kernel",
+    "repack_q4_kernel",
+}
+
+
+def test_kernel_list_is_the_product(lib):
+    """The device code object holds only the product's kernel families: kernel
+    descriptors are the `<mangled name>.kd` symbols of namespace lk."""
+    import ggml_hip._lib as L
+    blob = open(L.LIB_PATH, "rb").read()
+    names = re.findall(rb"_ZN2lk\d+([A-Za-z_0-9]+?_kernel)", blob)  # device symbols and host stubs
+    found = {m.decode().removeprefix("__device_stub__") for m in names}
+    assert found, "no lk:: kernels found in the library"
+    assert found <= PRODUCT_KERNELS, f"kernels outside the product set: {sorted(found - PRODUCT_KERNELS)}"
+    for k in ("gemv_stream_kernel", "gemm_skinny_pair_kernel", "gemm_wide_kernel", "xsplit_kernel"):
+        assert k in found
+
+
 def test_version_and_no_device(lib):
     assert b"gfx950" in lib.lk_version()
     import torch
