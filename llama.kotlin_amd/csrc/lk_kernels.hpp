@@ -637,7 +637,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     __builtin_amdgcn_s_barrier();  // ... and every other wave's
     }
 
-    // 2. activations into VGPRs in decode order, and Σx per block
+    // 2. activations into VGPRs in decode order, and Σx per block (only the node's own chunks:
+    //    a grouped launch runs every node at its largest node's class; A/B, four rounds: layer
+    //    launch 26.6 -> 26.3 us, chains unchanged)
     f32x4 xr[CPL][16];
     float xs0[CPL], xs1[CPL], xq[CPL][4];
     bool valid[CPL];
@@ -646,6 +648,15 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       const int p = c * 64 + lane;
       valid[c] = p < NP;
       const int pc = valid[c] ? p : 0;
+      if (c > 0 && c >= nch) {  // uniform: no lane of the chunk is valid (chunk 0 always is)
+#pragma unroll
+        for (int t = 0; t < 16; t++) xr[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        xs0[c] = xs1[c] = 0.f;
+        if constexpr (QT == LK_TYPE_Q2_K)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; g4++) xq[c][g4] = 0.f;
+        continue;
+      }
 #pragma unroll
       for (int jj = 0; jj < 8; jj++) {
         const f32x4 n0 = lds[16 * pc + ((2 * jj) ^ (pc & 15))], n1 = lds[16 * pc + ((2 * jj + 1) ^ (pc & 15))];
