@@ -250,19 +250,36 @@ def main():
         "roofline": roof,
     }
 
+    # the failure contract: a bounded in-launch wait that gave up is counted per
+    # section and reported here (lk_sync_timeouts also clears the flag the next synchronous entry
+    # point would raise on), so a section's result is never silently wrong and never blamed on
+    # the next section
+    waits = {"main": G.syncTimeouts()} if world == 1 else {}
+
+    def section(key, fn):
+        # a section whose synchronous call raised on a wait that gave up (LK_ERR_DEVICE) reports
+        # the error in its place instead of ending the run; the main line above has no such waits
+        try:
+            result[key] = fn()
+        except G.HipDeviceError as e:
+            result[key] = {"error": str(e)}
+        waits[key] = G.syncTimeouts()
+
     if rank == 0 and world == 1 and not args.no_chain:
-        result["decode_chain"] = decode_chain(torch, G, ga, nodes_by_layer, compute, token_bytes)
-        result["persistent_chain"] = {
+        section("decode_chain", lambda: decode_chain(torch, G, ga, nodes_by_layer, compute, token_bytes))
+        section("persistent_chain", lambda: {
             "layer_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 1),
-            "decode_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 4)}
+            "decode_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 4)})
     if rank == 0 and world == 1 and not args.no_headline:
-        result["headline_q4_0_4096x4096_n1"] = headline(torch, G, dev)
+        section("headline_q4_0_4096x4096_n1", lambda: headline(torch, G, dev))
     if rank == 0 and world == 1 and not args.no_batched:
-        result["n1_configs"] = n1_configs(torch, G, dev)
-        result["batched"] = batched(torch, G, dev)
-        result["next_rows"] = next_rows(torch, G, dev)
+        section("n1_configs", lambda: n1_configs(torch, G, dev))
+        section("batched", lambda: batched(torch, G, dev))
+        section("next_rows", lambda: next_rows(torch, G, dev))
     if rank == 0 and world == 1 and not args.no_host_path:
-        result["host_path_pcie"] = host_path(torch, G, dev)
+        section("host_path_pcie", lambda: host_path(torch, G, dev))
+    if waits:
+        result["sync_wait_timeouts"] = waits
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, token_bytes)
     if rank == 0:
