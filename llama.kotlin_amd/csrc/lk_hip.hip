@@ -904,7 +904,7 @@ int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
     static const bool kq_stream = [] { const char *e = getenv("LK_KQ_STREAM"); return !e || atoi(e) != 0; }();
     // Q2_K between 2K and 6K rows stays on kquant_n1_kernel: its 1344-B units leave the stream
     // kernel two per wave there, and the one-shot latency wins (4096^2: 5.45 vs 5.86 us; from
-    // 6144 rows on, and under 2K, the stream kernel is ahead: tools/lab/q2k_run.sh)
+    // 6144 rows on, and under 2K, the stream kernel is ahead: round-2 lab run q2k_run.sh)
     const bool q2k_mid = a->type == LK_TYPE_Q2_K && c.M > 2048 && c.M < 6144;
     if (kq_stream && !no_n1 && !q2k_mid && gemv_eligible(a, b, dst, c))
       if (const int cls = stream_class(a, c))

@@ -958,8 +958,8 @@ __device__ __forceinline__ void accumulate(f32x4 &acc, float s1, float s2, f32x4
 // acc += s1·p (+ s2·T for Q4_1) as four scalar FMAs: v_pk_fma_f32 beside MFMAs costs more
 // issue time than two v_fma_f32 (MI355X_MICROARCH.md, cycle constants), and the library is
 // built with -fno-slp-vectorize so the compiler does not pack these back.
-// A SIMD issues a wave64 v_pk_fma_f32 as fast as a v_fma_f32 (tools/lab/valu_rate.hip: ~4.3-4.7
-// cycles each at one or two waves per SIMD). Measured per kernel (tools/lab/pk_ab.sh, two boxes):
+// A SIMD issues a wave64 v_pk_fma_f32 as fast as a v_fma_f32 (round-2 lab tool valu_rate.hip, removed, see DESIGN §3: ~4.3-4.7
+// cycles each at one or two waves per SIMD). Measured per kernel (round-2 lab A/B pk_ab.sh, two boxes):
 // the wide GEMM runs C5 2-3 % faster with the packed form (accumulate), the wave-pair skinny
 // kernel 1-3 % slower, so each keeps its own.
 template <bool HAS_MIN>
@@ -1275,7 +1275,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_q_lds_kernel(GemmArgs g) {
 // C3's shape (M 11,008, K 4,096, N 32) is still bound by HBM (114 flop per weight byte). Its
 // weight stream only runs near HBM speed when each row's DMA piece is long — pieces that
 // straddle 128-B lines are fetched twice under `nt` (16 rows x 144 B stream at 3.8 TB/s,
-// 8 x 288 B at 5.6, 1 x 2,304 B at 6.3: tools/lab/pieces.hip) — and re-reading the
+// 8 x 288 B at 5.6, 1 x 2,304 B at 6.3: round-1 lab tool pieces.hip) — and re-reading the
 // activations per 16-row tile from LDS left every block waiting on an LDS round trip. So:
 //
 //   workgroup (range r, slice s): rows of range r x blocks [s·SB, s·SB + SB) of K, one wave

@@ -14,7 +14,7 @@
 //    (exact f32 products) straight into the accumulators.
 //
 // On gfx950 a SIMD issues one wave64 VALU instruction per ~4.3 cycles whether one or two waves
-// share it (tools/lab/valu_rate.hip), so the VALU count per block, not latency, sets the pace:
+// share it (round-2 lab tool valu_rate.hip, removed), so the VALU count per block, not latency, sets the pace:
 // 8 + 1 + NT·2 VALU per block here against ~25 for the fp8-conversion decode with scalar FMAs.
 //
 // Schedule: workgroup = (row range, K slice of 16 blocks), 8 waves; wave (stream p = w % 4,
