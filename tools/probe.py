@@ -7,6 +7,7 @@ Sections (default: all):
   n1       Q4_0 4096^2 / 11008x4096 / 4096x11008 single launches at batch 1 (rotating copies)
   c3       Q4_0 / Q4_1 11008x4096 at N = 32
   c5       Q4_0 4096^2 at N = 512
+  c1       F32 512^3 (the general F32 path on the f32 MFMA)
 Every time is the mean over a HIP-graph replay (bench._graph_time)."""
 import json
 import os
@@ -21,7 +22,7 @@ import bench  # noqa: E402
 def main():
     import torch
     import ggml_hip as G
-    want = set(sys.argv[1:]) or {"layer", "chain", "n1", "c3", "c5"}
+    want = set(sys.argv[1:]) or {"layer", "chain", "n1", "c3", "c5", "c1"}
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     G.load_library()
@@ -71,17 +72,20 @@ def main():
         out["c3_q4_1"] = _single(torch, G, dev, s, T.Q4_1, 11008, 4096, 32, 16)
     if "c5" in want:
         out["c5_q4_0"] = _single(torch, G, dev, s, T.Q4_0, 4096, 4096, 512, 32)
+    if "c1" in want:
+        out["c1_f32"] = _single(torch, G, dev, s, T.F32, 512, 512, 512, 4)
     print(json.dumps(out), flush=True)
 
 
 def _single(torch, G, dev, s, qt, M, K, N, copies):
     T = G.GGMLType
-    nb = M * K // 32 * G.GGMLType(qt).byteSize
+    nb = M * K * 4 if qt == T.F32 else M * K // 32 * G.GGMLType(qt).byteSize
     g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
     wb, xb, db = g.addBuffer(copies * nb + 256), g.addBuffer(4 * K * N + 256), g.addBuffer(4 * M * N * copies + 256)
     src = torch.randn(M * K, device=dev) * 0.02
     for c in range(copies):
-        g.buffers[wb][c * nb:(c + 1) * nb].copy_(G.quantizeTensor(src * (1 + 0.01 * c), qt))
+        g.buffers[wb][c * nb:(c + 1) * nb].copy_((src * (1 + 0.01 * c)).view(torch.uint8) if qt == T.F32
+                                                 else G.quantizeTensor(src * (1 + 0.01 * c), qt))
     g.buffers[xb][: 4 * K * N].copy_(torch.randn(K * N, device=dev).view(torch.uint8))
     nodes = [(G.GGMLTensor(qt, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [N, K], bufferId=xb),
               G.GGMLTensor(T.F32, [N, M], bufferId=db, dataOffset=4 * M * N * c)) for c in range(copies)]
