@@ -745,7 +745,7 @@ def batched(torch, G, dev, reps=10):
     torch.cuda.synchronize()
     per = e0.elapsed_time(e1) / 1e3 / (reps * copies)
     out["c1_f32_512x512x512"] = {"avg_launch_us": round(per * 1e6, 3), "GFLOPs": round(2 * n ** 3 / per / 1e9, 1),
-                                 "kernel": "f32_mfma_kernel (general F32 path, computeMatMul :1530-1543, on v_mfma_f32_32x32x2_f32)", "hip_graph": gr is not None}
+                                 "kernel": "f32_lds_kernel (general F32 path, computeMatMul :1530-1543, operands staged in LDS, on v_mfma_f32_32x32x2_f32)", "hip_graph": gr is not None}
     del g
     return out
 

@@ -833,7 +833,11 @@ int launch_f32_mfma(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, cons
   if (gx > 0x7FFFFFFF || gy > 65535) return launch_generic(a, b, dst, c, st);
   dim3 grid((unsigned)gx, (unsigned)gy), block(256);
   const bool v4 = g.a_nb0 == 4 && g.a_nb1 % 16 == 0 && ((uintptr_t)g.a & 15) == 0;
-  if (v4) hipLaunchKernelGGL(f32_mfma_kernel<true>, grid, block, 0, st, g);
+  const bool dense = v4 && g.b_nb0 == 4 && g.b_nb1 % 16 == 0 && ((uintptr_t)g.b & 15) == 0 && c.K % kF32Chunk == 0 &&
+                     c.N % 4 == 0 && (c.M - 1) * g.a_nb1 + 4 * c.K < (1ll << 32) && c.K * g.b_nb1 < (1ll << 32) &&
+                     !getenv_flag("LK_F32_DIRECT");
+  if (dense) hipLaunchKernelGGL(f32_lds_kernel, grid, block, 4 * 32768, st, g);
+  else if (v4) hipLaunchKernelGGL(f32_mfma_kernel<true>, grid, block, 0, st, g);
   else hipLaunchKernelGGL(f32_mfma_kernel<false>, grid, block, 0, st, g);
   HIP_TRY(hipGetLastError());
   return LK_OK;

@@ -2415,6 +2415,69 @@ __global__ __launch_bounds__(256) void f32_mfma_kernel(GenericArgs g) {
   }
 }
 
+// Dense variant (C1): the same tiles and K split, operands staged in LDS by LDS-DMA in whole
+// 16-B pieces (A: row pieces XOR-swizzled by row, so the 16 rows of a ds_read_b128 lane group hit
+// distinct bank slots; B: k rows of the tile's 32 columns), then read per MFMA step from LDS —
+// instead of per-lane strided global loads (each A load instruction touched 64 lines). Needs
+// K % 128 == 0, A rows and B k rows 16-B aligned, N % 4 == 0; rows / columns past M / N re-read
+// the last valid ones and are never stored.
+constexpr int kF32Chunk = 128;  // k per wave and chunk
+__global__ __launch_bounds__(256) void f32_lds_kernel(GenericArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t i0 = (int64_t)blockIdx.y * 32, j0 = (int64_t)blockIdx.x * 32;
+  uint8_t *abuf = smem + wave * 32768, *bbuf = abuf + 16384;  // this wave's A (2 x 32 x 64) and B (128 x 32)
+  f32x16_t acc = {};
+  for (int64_t kc = (int64_t)wave * kF32Chunk; kc < g.K; kc += 4 * kF32Chunk) {
+    // two halves of 64 k, each A [32 rows][16 pieces] then B [64 k][32 columns]: the first half's
+    // MFMAs run while the second half lands
+#pragma unroll
+    for (int hf = 0; hf < 2; hf++) {
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const int q = t * 64 + lane, ar = q >> 4, cp = (q & 15) ^ (ar & 15);  // A: row ar, piece cp
+        const int64_t ai = min(i0 + ar, g.M - 1);
+        dma16<false>(g.a, (uint32_t)(ai * g.a_nb1 + (kc + 64 * hf + 4 * cp) * 4), abuf + hf * 8192 + t * 1024);
+      }
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const int q = t * 64 + lane, bk = q >> 3, c = q & 7;  // B: k row bk, columns j0 + 4c ..
+        const int64_t bj = min(j0 + 4 * c, g.N - 4);
+        dma16<false>(g.b, (uint32_t)((kc + 64 * hf + bk) * g.b_nb1 + bj * 4), bbuf + hf * 8192 + t * 1024);
+      }
+    }
+#pragma unroll
+    for (int hf = 0; hf < 2; hf++) {
+      if (hf == 0) wait_vmcnt<16>();
+      else wait_vmcnt<0>();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int s4 = 0; s4 < 8; s4++) {  // MFMA steps 4·s4 .. +3: lane half h supplies k = 64·hf + 32h + s
+        const int piece = 8 * h + s4;
+        const f32x4 av = *(const f32x4 *)(abuf + hf * 8192 + r * 256 + ((piece ^ (r & 15)) * 16));
+        const float *bp = (const float *)(bbuf + hf * 8192 + (32 * h + 4 * s4) * 128) + r;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bp[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bp[32], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bp[64], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bp[96], acc, 0, 0, 0);
+      }
+    }
+    wait_lgkmcnt0();  // this chunk's LDS reads are done before the next chunk's DMA overwrites it
+  }
+  __syncthreads();
+  float *red = (float *)smem;  // [4][16][64], over the (now idle) staging area
+#pragma unroll
+  for (int q = 0; q < 16; q++) red[(wave * 16 + q) * 64 + lane] = acc[q];
+  __syncthreads();
+  for (int e = (int)threadIdx.x; e < 16 * 64; e += 256) {  // waves summed in order (deterministic)
+    const int q = e >> 6, l = e & 63;
+    const float v = ((red[q * 64 + l] + red[(16 + q) * 64 + l]) + red[(32 + q) * 64 + l]) + red[(48 + q) * 64 + l];
+    const int64_t ii = i0 + (q & 3) + 8 * (q >> 2) + 4 * (l >> 5), jj = j0 + (l & 31);
+    if (ii < g.M && jj < g.N) *(float *)(g.dst + jj * g.d_nb0 + ii * g.d_nb1) = v;
+  }
+}
+
 // ---- generic path (any K, any byte strides, ragged blocks) ----------------------
 
 

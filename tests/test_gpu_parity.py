@@ -410,6 +410,30 @@ def test_wide_gemm_vs_oracle(gpu, oracle, qt, shape):
     assert ok, ("strided dst", msg)
 
 
+@pytest.mark.parametrize("shape", [(100, 1024, 36), (33, 128, 4), (257, 384, 60), (64, 4096, 32)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_f32_lds_kernel_edges(gpu, oracle, shape):
+    """The LDS-staged F32 MFMA kernel (dense operands, K % 128 == 0, N % 4 == 0): ragged rows and
+    columns (re-read, never stored), one chunk for one of four waves, several chunks per wave;
+    against the oracle (F32 path, GGMLComputeOps.kt:1530-1543) and bit-equal on a rerun."""
+    import ggml_hip as G
+    M, K, N = shape
+    a = pattern_f32(M * K, 3)
+    x = pattern_f32(K * N, 4)
+    ref = oracle.mat_mul_q(oracle.F32, a.view(np.uint8), M, K, x.reshape(K, N))
+    outs = []
+    for _ in range(2):
+        ga = G.GGMLGraphAllocator(defaultBufferSize=4 * (M * K + K * N + M * N) + 1024)
+        ta = ga.allocateTensor(G.GGMLType.F32, [K, M]); ga.setTensorBytes(ta, a)
+        tb = ga.allocateTensor(G.GGMLType.F32, [N, K]); ga.setTensorBytes(tb, x)
+        td = ga.allocateTensor(G.GGMLType.F32, [N, M])
+        G.computeMatMul(ga, ga.context, ta, tb, td)
+        outs.append(ga.tensorBytes(td).cpu().numpy().view(np.float32).reshape(M, N).copy())
+    ok, msg = parity_ok(outs[0], ref, noise=acc_noise(np.abs(a.reshape(M, K)), np.abs(x.reshape(K, N))))
+    assert ok, msg
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
 def test_c1_f32_512_cubed(gpu, oracle):
     """BASELINE config C1 at its size: F32 512x512x512 through computeMatMul's general path
     (GGMLComputeOps.kt:1530-1543), the benchmark test's F32 values
