@@ -1299,10 +1299,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_q_lds_kernel(GemmArgs g) {
 // dword its blocks need (WPB per block) with one burst of LDS reads and one wait.
 
 // Weight DMA policy of the skinny GEMM: default (0) keeps lines in L2, where the neighbouring
-// slice's workgroup (same XCD) reads the 128-B line its piece shares with this one. The wave-pair
-// kernel (C3) streams with nt instead: A/B, three rounds, C3 Q4_0 20.6 -> 20.2 us, Q4_1
-// 20.6-20.8 -> 20.0-20.4 us (nt on gemm_wide_kernel's weight pieces, which every CU of a row band
-// re-reads from L2, was 15 % slower: C5 53.3 -> 61.5 us).
+// slice's workgroup (same XCD) reads the 128-B line its piece shares with this one. Measured
+// instead, the skinny kernels stream with nt: A/B, three rounds, wave-pair kernel C3 Q4_0
+// 20.6 -> 20.2 us, Q4_1 20.6-20.8 -> 20.0-20.4 us; one-wave kernel Q4_0 11008x4096 N = 8
+// 16.5-17.0 -> 16.3 us, N = 16 16.7-17.3 -> 16.4-16.7 us (nt on gemm_wide_kernel's weight pieces,
+// which every CU of a row band re-reads from L2, was 15 % slower: C5 53.3 -> 61.5 us).
 
 template <int QT, int NT> struct SkinnyGeom {
   static constexpr int NW = 4;                         // waves per workgroup: one per SIMD
@@ -1572,7 +1573,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
 #pragma unroll
     for (int j = 0; j < L; j++) {
       const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
-      dma16<0>(tb, vofs, ring + sl * G::SLOT + j * 1024);
+      dma16<1>(tb, vofs, ring + sl * G::SLOT + j * 1024);  // nt: read once per launch
     }
   };
   // 1. the HBM stream starts with one unit per wave

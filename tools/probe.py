@@ -8,6 +8,7 @@ Sections (default: all):
   c3       Q4_0 / Q4_1 11008x4096 at N = 32
   c5       Q4_0 4096^2 at N = 512
   c1       F32 512^3 (the general F32 path on the f32 MFMA)
+  skinny   Q4_0 11008x4096 at N = 8 and 16 (gemm_skinny_kernel)
 Every time is the mean over a HIP-graph replay (bench._graph_time)."""
 import json
 import os
@@ -72,6 +73,9 @@ def main():
         out["c3_q4_1"] = _single(torch, G, dev, s, T.Q4_1, 11008, 4096, 32, 16)
     if "c5" in want:
         out["c5_q4_0"] = _single(torch, G, dev, s, T.Q4_0, 4096, 4096, 512, 32)
+    if "skinny" in want:
+        out["q4_0_n8"] = _single(torch, G, dev, s, T.Q4_0, 11008, 4096, 8, 16)
+        out["q4_0_n16"] = _single(torch, G, dev, s, T.Q4_0, 11008, 4096, 16, 16)
     if "c1" in want:
         out["c1_f32"] = _single(torch, G, dev, s, T.F32, 512, 512, 512, 4)
     print(json.dumps(out), flush=True)
