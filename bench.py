@@ -18,6 +18,14 @@ Multi-GPU (one process per GPU): every weight matrix is row-sharded (rank r owns
 [r·M/P, (r+1)·M/P)); each layer is one lk_sharded_plan of the C-ABI — the local rows computed in
 place inside the full output buffers, then one RCCL group of in-place all-gathers over xGMI — and
 the next layer reads the gathered outputs. Total work per step is fixed -> "scaling": "strong".
+`--sharded` takes that path at one rank too (start it under `torchrun --nproc-per-node 1`): the
+C-ABI communicator is built from a world-1 NCCL process group and each layer is a one-rank
+lk_sharded_plan with its RCCL group of in-place gathers, captured in the HIP graph — the exact
+code the 8-GPU run executes, measured on one GPU (its value should match the plain line).
+
+Exit status: the JSON line is always printed; the run exits 3 afterwards when any section reports
+an error or any bounded in-launch wait gave up (sync_wait_timeouts), so a driver never takes a
+partial line for a clean one.
 
 value = whole-job algorithmic GB/s = Σ_nodes (M·K/32·18 + 4·K + 4·M) bytes per token x
 tokens / wall time (max over ranks). tokens_per_s is reported beside it.
@@ -84,6 +92,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=6144)
+    ap.add_argument("--sharded", action="store_true",
+                    help="the N > 1 path (C-ABI RCCL communicator + lk_sharded_plan) at any world size")
     args = ap.parse_args()
 
     import torch
@@ -99,7 +109,8 @@ def main():
         local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or args.sharded
+    if distributed:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -155,7 +166,7 @@ def main():
     # layer L+1 reads layer L's outputs, so at N > 1 each layer's RCCL all-gather (in the C-ABI,
     # lk_sharded_plan) sits on the path between consecutive layers
     comm = None
-    if world > 1 and backend == "nccl":
+    if distributed and backend == "nccl":
         # the C-ABI's RCCL path is the product: if it cannot be set up the run fails (no fallback)
         comm = G.Comm.from_process_group()
         plans = [[G.ShardedMulMatPlan(comm, ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
@@ -195,7 +206,7 @@ def main():
     with torch.cuda.stream(compute):
         run()  # one untimed replay (graph upload)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -206,12 +217,12 @@ def main():
             run()
         ev1.record(compute)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -244,7 +255,7 @@ def main():
                                "reads layer L's outputs (at N > 1 after the in-place RCCL all-gather); the "
                                "intra-layer dependent decode schedule is decode_chain",
                    "parallelism": (f"row-shard{world}+{'rccl-c-abi' if comm is not None else 'torch-' + backend}-allgather"
-                                   if world > 1 else "single"),
+                                   if distributed else "single"),
                    "launches_per_step_per_rank": launches_per_step, "hip_graph": graph is not None,
                    "gpu_ms_per_step": round(ev_ms / args.steps, 4)},
         "roofline": roof,
@@ -282,9 +293,13 @@ def main():
         result["sync_wait_timeouts"] = waits
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, token_bytes)
+    failed = [k for k, v in result.items() if isinstance(v, dict) and "error" in v]
+    failed += [f"sync_wait_timeouts.{k}" for k, v in waits.items() if v]
+    if failed:
+        result["failed_sections"] = failed
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         for lp in plans:
             for p in lp:
@@ -292,6 +307,9 @@ def main():
         if comm is not None:
             comm.close()
         dist.destroy_process_group()
+    if failed:
+        print(f"[bench] failed sections: {failed}", file=sys.stderr)
+        sys.exit(3)
 
 
 def roofline(torch, plans, local_by_layer, stream, world, reps=10):

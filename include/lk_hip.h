@@ -233,6 +233,11 @@ int lk_comm_device(const lk_comm *comm);
  * captured ones does not count again). */
 uint64_t lk_comm_num_collectives(const lk_comm *comm);
 void lk_comm_destroy(lk_comm *comm);
+/* Tears down the communicator's enqueued collectives (ncclCommAbort), e.g. after a failure left
+ * some ranks' all-gathers waiting for peers that never arrive; later collectives through it fail
+ * with LK_ERR_DEVICE. The handle still needs lk_comm_destroy. A failure inside an RCCL group
+ * aborts the communicators involved itself (a sharded graph then refuses further computes). */
+int lk_comm_abort(lk_comm *comm);
 int lk_comm_group_start(void);
 int lk_comm_group_end(void);
 

@@ -113,6 +113,18 @@ int lk_comm_rank(const lk_comm *c) { return c ? c->rank : -1; }
 int lk_comm_device(const lk_comm *c) { return c ? c->device : -1; }
 uint64_t lk_comm_num_collectives(const lk_comm *c) { return c ? c->collectives : 0; }
 
+// Tears down the communicator's enqueued collectives (ncclCommAbort): after a failure left some
+// ranks' collectives waiting for peers that never arrive. The handle stays valid for
+// lk_comm_destroy; any later collective through it fails.
+int lk_comm_abort(lk_comm *c) {
+  if (!c) return lk_detail_fail(LK_ERR_INVALID_ARG, "comm: null");
+  if (!c->comm) return LK_OK;
+  const ncclResult_t r = ncclCommAbort(c->comm);
+  c->comm = nullptr;
+  if (r != ncclSuccess) return failf(LK_ERR_DEVICE, "ncclCommAbort", r);
+  return LK_OK;
+}
+
 void lk_comm_destroy(lk_comm *c) {
   if (!c) return;
   if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -173,6 +185,7 @@ int lk_sharded_plan_create(lk_comm *comm, const lk_tensor *a, const lk_tensor *b
 int lk_sharded_plan_launch(lk_sharded_plan *p, void *stream) {
   if (!p) return lk_detail_fail(LK_ERR_INVALID_ARG, "null sharded plan");
   hipStream_t st = (hipStream_t)stream;
+  if (!p->comm->comm) return lk_detail_fail(LK_ERR_DEVICE, "sharded plan: its communicator was aborted");
   return on_device(p->comm->device, [&]() -> int {
     int rc = lk_plan_launch(p->local, stream);
     if (rc) return rc;
@@ -183,7 +196,9 @@ int lk_sharded_plan_launch(lk_sharded_plan *p, void *stream) {
       const ncclResult_t r = ncclAllGather(full + (uint64_t)p->comm->rank * g.chunk, full, g.chunk, ncclChar,
                                            p->comm->comm, st);
       if (r != ncclSuccess) {
+        // part of this rank's gathers may be enqueued, waiting for peers: tear them down
         (void)ncclGroupEnd();
+        (void)lk_comm_abort(p->comm);
         return failf(LK_ERR_DEVICE, "ncclAllGather", r);
       }
       p->comm->collectives++;

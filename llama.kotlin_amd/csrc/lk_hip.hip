@@ -89,6 +89,7 @@ using MirrorRef = std::shared_ptr<Mirror>;
 struct Dev {
   hipStream_t stream = nullptr;
   unsigned *fail_flag = nullptr;  // page-locked word behind lk_sync_fail_flag (lk_kernels.hpp)
+  unsigned timeouts_seen = 0;     // lk_sync_timeout_count at the last lk_sync_timeouts
   // weight residency cache (host path): the current mirrors of this device (guarded by S().cache_mu)
   std::vector<MirrorRef> weights;
   uint64_t weight_bytes = 0;
@@ -381,10 +382,9 @@ struct GemmScratch {
   void *frag = nullptr; size_t frag_bytes = 0;
   void *partial = nullptr; size_t partial_bytes = 0;
   int32_t *counter = nullptr; size_t counter_n = 0;
-  unsigned *rsync = nullptr;  // fused split-K arrival counters: kRsyncRows rows of rsync_line lines
-  int rsync_line = 0;
+  unsigned *tcnt = nullptr;  // split-K arrival counters, one word per output tile of a launch
+  size_t tcnt_n = 0;
 };
-constexpr int kRsyncRows = 64;  // slices values 1..64 (K <= 32768 on the skinny path)
 
 GemmScratch &gemm_scratch() {
   static GemmScratch per_dev[64];
@@ -392,24 +392,26 @@ GemmScratch &gemm_scratch() {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   return per_dev[dev];
 }
-// Fused split-K reduction (lk_kernels.hpp splitk_fused_reduce) for `slices` slices of slab_bytes:
-// the counter row to pass, or null (splitk_reduce_kernel runs after: LK_SKP_UNFUSED=1, one slice,
-// too many slices, or slabs beyond a 32-bit buffer offset). The caller keeps ranges·slices <=
-// cu_count() so every task is co-resident (one workgroup per CU).
-int fused_rsync(int slices, size_t slab_bytes, unsigned **out) {
+// Split-K fix-up by the last arriver (lk_kernels.hpp splitk_arrive): the per-tile arrival counters
+// to pass (ntiles words, zero between launches: the last arrival of each tile re-arms its word), or
+// null — then splitk_reduce_kernel sums the slabs after the GEMM (LK_SKP_UNFUSED=1, one slice, slabs
+// beyond a 32-bit buffer offset, or more tiles per workgroup than its LDS list holds: list_ok false).
+// No co-residency is assumed: nobody waits, so any grid size and any concurrent stream are safe.
+int splitk_counters(int slices, size_t slab_bytes, int64_t ntiles, bool list_ok, unsigned **out) {
   static const bool unfused = getenv("LK_SKP_UNFUSED") != nullptr;
   *out = nullptr;
-  const int cu = cu_count();
-  if (unfused || slices <= 1 || slices > kRsyncRows || slices > cu || slab_bytes >= (1ull << 31)) return LK_OK;
+  if (unfused || slices <= 1 || !list_ok || slab_bytes >= (1ull << 31) || ntiles <= 0) return LK_OK;
   GemmScratch &S = gemm_scratch();
-  if (!S.rsync) {
-    const int line = (cu + 7) / 8 * 8;  // a line per range: arrivals (word 0), departures (word 1)
-    const size_t bytes = (size_t)kRsyncRows * line * kChainLine * sizeof(unsigned);
-    HIP_TRY(hipMalloc((void **)&S.rsync, bytes));
-    HIP_TRY(hipMemset(S.rsync, 0, bytes));
-    S.rsync_line = line;
+  if (S.tcnt_n < (size_t)ntiles) {
+    const size_t want = std::max<size_t>((size_t)ntiles, 1 << 14);
+    if (S.tcnt) HIP_TRY(hipFree(S.tcnt));
+    S.tcnt = nullptr;
+    S.tcnt_n = 0;
+    HIP_TRY(hipMalloc((void **)&S.tcnt, want * sizeof(unsigned)));
+    HIP_TRY(hipMemset(S.tcnt, 0, want * sizeof(unsigned)));
+    S.tcnt_n = want;
   }
-  *out = S.rsync + (size_t)(slices - 1) * S.rsync_line * kChainLine;
+  *out = S.tcnt;
   return LK_OK;
 }
 
@@ -558,14 +560,15 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
   const int nblk = g.K / 32;
   const int slices = (nblk + SG::SB - 1) / SG::SB;
   const int ntile = (g.M + 15) / 16;
-  // one workgroup per CU (LDS): about cu_count() workgroups in all; fused split-K reduction
-  // unless LK_SKP_UNFUSED=1 (every task co-resident)
+  // one workgroup per CU (LDS): about cu_count() workgroups in all; split-K fixed up by the last
+  // arriver per tile unless LK_SKP_UNFUSED=1 (its list: 16 + NW·⌈tiles/NW⌉ ints in the staging area)
   const int cu = cu_count();
-  unsigned *rsync = nullptr;
-  if (int rf = fused_rsync(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), &rsync)) return rf;
-  int ranges = std::max(1, std::min(ntile, rsync ? cu / slices : (cu + slices - 1) / slices));
+  int ranges = std::max(1, std::min(ntile, cu / slices));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
+  unsigned *rsync = nullptr;
+  const bool list_ok = 16 + SG::NW * ((g.tiles_per_range + SG::NW - 1) / SG::NW) <= SG::XB / 4;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, &rsync)) return rf;
   g.slices = slices;
   if (slices > 1) {
     const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
@@ -593,15 +596,16 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   const int nblk = g.K / 32;
   const int slices = (nblk + SG::SB - 1) / SG::SB;
   const int ntile = (g.M + 15) / 16;
-  // fused split-K reduction unless LK_SKP_UNFUSED=1 (fused_rsync): every task co-resident
+  // split-K fixed up by the last arriver per tile unless LK_SKP_UNFUSED=1 (splitk_counters)
   const int cu = cu_count();
   const size_t slab_bytes = (size_t)slices * g.M * 16 * NT * sizeof(float);
-  unsigned *rsync = nullptr;
-  if (int rc = fused_rsync(slices, slab_bytes, &rsync)) return rc;
-  const bool fuse = rsync != nullptr;
-  int ranges = std::max(1, std::min(ntile, fuse ? cu / slices : (cu + slices - 1) / slices));
+  int ranges = std::max(1, std::min(ntile, cu / slices));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
+  unsigned *rsync = nullptr;
+  const bool list_ok = 16 + 4 * ((g.tiles_per_range + 3) / 4) <= SG::XB / 4;
+  if (int rc = splitk_counters(slices, slab_bytes, ntile, list_ok, &rsync)) return rc;
+  const bool fuse = rsync != nullptr;
   g.slices = slices;
   if (slices > 1) {
     const int rc = grow(&S.partial, &S.partial_bytes, slab_bytes);
@@ -623,7 +627,7 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
 
 // gemm_sk_kernel (lk_skinny.hpp): Q4_K x F32, 16 <= N <= 32. Dense, 16-B aligned activations
 // are split by the kernel itself; others go through xsplit_kernel first. Split-K slabs are
-// reduced inside the launch (fused_rsync) or by splitk_reduce_kernel after it.
+// fixed up inside the launch by the last arriver per tile (splitk_counters) or by splitk_reduce_kernel after it.
 template <int QT, int NT>
 int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   using SG = SkGeom<QT, NT>;
@@ -650,11 +654,12 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   const int slices = (int)((nblk + SG::SB - 1) / SG::SB);
   const int ntile = (g.M + 15) / 16;
   const int cu = cu_count();
-  unsigned *rsync = nullptr;
-  if (int rf = fused_rsync(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), &rsync)) return rf;
-  int ranges = std::max(1, std::min(ntile, rsync ? cu / slices : (cu + slices - 1) / slices));
+  int ranges = std::max(1, std::min(ntile, cu / slices));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
+  unsigned *rsync = nullptr;
+  const bool list_ok = 16 + 4 * ((g.tiles_per_range + 3) / 4) <= SG::XF / 4;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, &rsync)) return rf;
   g.slices = slices;
   if (slices > 1) {
     rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
@@ -745,10 +750,9 @@ int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
   g.sm = std::min(g.tiles_m, (per_xcd + best - 1) / best);
   const int nsuper = ((g.tiles_m + g.sm - 1) / g.sm) * ((g.tiles_n + g.sn - 1) / g.sn);
   g.tasks = nsuper * g.sm * g.sn * slices;
-  // fused split-K reduction in gemm_wide_kernel when every task is co-resident (one per CU)
+  // split-K fixed up inside gemm_wide_kernel by the last arriver per tile (splitk_counters)
   g.rsync = nullptr;
-  if (g.tasks <= cu_count())
-    if (int rf = fused_rsync(slices, (size_t)slices * g.M * npad * sizeof(float), &g.rsync)) return rf;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * npad * sizeof(float), tiles, true, &g.rsync)) return rf;
   launch_xsplit(xa, st);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
@@ -820,7 +824,7 @@ GenericArgs make_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst,
 
 int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st);
 
-bool getenv_flag(const char *name) {  // lab switches, read per call (cheap; A/B only)
+bool getenv_flag(const char *name) {  // lab switches (A/B only): callers read them once into a static
   const char *e = getenv(name);
   return e && *e && *e != '0';
 }
@@ -828,6 +832,7 @@ bool getenv_flag(const char *name) {  // lab switches, read per call (cheap; A/B
 // F32 x F32 -> F32 on the f32 MFMA (f32_mfma_kernel): any strides; float4 loads of A's rows when
 // they are contiguous and 16-byte aligned.
 int launch_f32_mfma(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  static const bool f32_direct = getenv_flag("LK_F32_DIRECT");
   const GenericArgs g = make_generic(a, b, dst, c);
   const int64_t gx = (c.N + 31) / 32, gy = (c.M + 31) / 32;
   if (gx > 0x7FFFFFFF || gy > 65535) return launch_generic(a, b, dst, c, st);
@@ -835,7 +840,7 @@ int launch_f32_mfma(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, cons
   const bool v4 = g.a_nb0 == 4 && g.a_nb1 % 16 == 0 && ((uintptr_t)g.a & 15) == 0;
   const bool dense = v4 && g.b_nb0 == 4 && g.b_nb1 % 16 == 0 && ((uintptr_t)g.b & 15) == 0 && c.K % kF32Chunk == 0 &&
                      c.N % 4 == 0 && (c.M - 1) * g.a_nb1 + 4 * c.K < (1ll << 32) && c.K * g.b_nb1 < (1ll << 32) &&
-                     !getenv_flag("LK_F32_DIRECT");
+                     !f32_direct;
   if (dense) hipLaunchKernelGGL(f32_lds_kernel, grid, block, 4 * 32768, st, g);
   else if (v4) hipLaunchKernelGGL(f32_mfma_kernel<true>, grid, block, 0, st, g);
   else hipLaunchKernelGGL(f32_mfma_kernel<false>, grid, block, 0, st, g);
@@ -987,7 +992,8 @@ int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *ds
     return launch_generic(a, b, dst, c, st);
   }
   if (c.path == Path::kKQuantF32) return launch_kquant(a, b, dst, c, st);
-  if (c.path == Path::kF32 && !getenv_flag("LK_NO_F32_MFMA")) return launch_f32_mfma(a, b, dst, c, st);
+  static const bool no_f32_mfma = getenv_flag("LK_NO_F32_MFMA");
+  if (c.path == Path::kF32 && !no_f32_mfma) return launch_f32_mfma(a, b, dst, c, st);
   if (gemv_eligible(a, b, dst, c)) return run_single_gemv(a, b, dst, c, st);
   if (gemm_eligible(c)) return skinny_eligible(a, c) ? launch_skinny(a, b, dst, c, st) : launch_gemm(a, b, dst, c, st);
   return launch_generic(a, b, dst, c, st);
@@ -1028,12 +1034,19 @@ int init_dev(int d) {
   return LK_OK;
 }
 
-// After a host synchronisation of device d: LK_ERR_DEVICE (and the flag re-armed) when one of the
-// device-side waits of the launches since the last check gave up — their results are undefined.
-int sync_failures(int d) {
+// The failure word of device d before a synchronous entry point's launches (lk_note_timeout
+// stores the device's running count of waits that gave up into it).
+unsigned fail_mark(int d) {
   Dev &v = S().devs[d];
-  if (!v.fail_flag || !__atomic_load_n(v.fail_flag, __ATOMIC_ACQUIRE)) return LK_OK;
-  __atomic_store_n(v.fail_flag, 0u, __ATOMIC_RELEASE);
+  return v.fail_flag ? __atomic_load_n(v.fail_flag, __ATOMIC_ACQUIRE) : 0u;
+}
+
+// After a host synchronisation of device d: LK_ERR_DEVICE when the word moved since `before`,
+// i.e. a device-side wait gave up while this call's launches ran — their results are undefined.
+// Each call compares against its own mark, so a failure is never consumed by another thread's
+// call (a concurrent failure on the same device may be reported by both).
+int sync_failures(int d, unsigned before) {
+  if (fail_mark(d) == before) return LK_OK;
   return fail(LK_ERR_DEVICE,
               "device %d: a split-K or chain wait gave up at its bound (workgroups not co-resident: another launch "
               "shares the GPU); the results of that launch are undefined", d);
@@ -1228,6 +1241,7 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   if (rc) return rc;
   Dev &s = cur();
   hipStream_t st = s.stream;
+  const unsigned mark = fail_mark(S().device);
   const uint64_t a_bytes = c.a_hi - c.a_lo, b_bytes = c.b_hi - c.b_lo, d_bytes = c.d_hi - c.d_lo;
   // A: cached mirror or staged copy
   const MirrorRef pinned = find_pinned(s, a->data, c.a_lo, c.a_hi);  // held for the call
@@ -1252,7 +1266,7 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync((uint8_t *)dst->data + c.d_lo, s.scratch[2], d_bytes, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  return sync_failures(S().device);
+  return sync_failures(S().device, mark);
 }
 
 // ---- row-sharded host operator: one process, several GPUs (SURVEY §8b lk_mul_mat_sharded) -----
@@ -1348,9 +1362,11 @@ int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, i
   const uint64_t b_bytes = c.b_hi - c.b_lo;
   std::vector<uint64_t> a_need(ndev, 0), d_need(ndev, 0);
   std::vector<char> used(ndev, 0);
+  std::vector<unsigned> mark(ndev, 0);
   for (auto &x : sh) {
     if ((rc = init_dev(x.dev))) goto out;
     Dev &v = S().devs[x.dev];
+    if (!used[x.dev]) mark[x.dev] = fail_mark(x.dev);
     used[x.dev] = 1;
     x.pin = find_pinned(v, a->data, x.c.a_lo, x.c.a_hi);
     x.a_dev = x.pin ? (const uint8_t *)x.pin->ptr + (x.c.a_lo - x.pin->lo) : nullptr;
@@ -1400,7 +1416,7 @@ int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, i
     if (used[d] && hipStreamSynchronize(S().devs[d].stream) != hipSuccess && rc == LK_OK)
       rc = fail(LK_ERR_DEVICE, "sharded: device %d failed", d);
   for (int d = 0; d < ndev; d++)
-    if (used[d] && rc == LK_OK) rc = sync_failures(d);
+    if (used[d] && rc == LK_OK) rc = sync_failures(d, mark[d]);
 out:
   (void)hipSetDevice(prev);
   return rc;
@@ -1665,7 +1681,6 @@ int lk_plan_chain_timed_out(lk_plan *plan) {
   if (hipMemcpy(&flag, plan->sync + words - kChainLine, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess) return fail(LK_ERR_DEVICE, "chain: flag");
   if (flag) {
     (void)hipMemset(plan->sync, 0, (size_t)words * sizeof(unsigned));
-    (void)sync_failures(S().device);  // reported here instead
     return 1;
   }
   return 0;
@@ -1676,13 +1691,12 @@ int lk_sync_timeouts(uint32_t *count) {
   int rc = ensure_init();
   if (rc) return rc;
   unsigned v = 0;
-  const unsigned zero = 0;
   if (hipDeviceSynchronize() != hipSuccess) return fail(LK_ERR_DEVICE, "sync");
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(lk_sync_timeout_count), sizeof(v)) != hipSuccess ||
-      hipMemcpyToSymbol(HIP_SYMBOL(lk_sync_timeout_count), &zero, sizeof(zero)) != hipSuccess)
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(lk_sync_timeout_count), sizeof(v)) != hipSuccess)
     return fail(LK_ERR_DEVICE, "timeout count");
-  (void)sync_failures(S().device);  // reported here instead
-  *count = v;
+  Dev &d = cur();  // the device count is monotonic: report the increase since the last call
+  *count = v - d.timeouts_seen;
+  d.timeouts_seen = v;
   return LK_OK;
 }
 
@@ -1700,10 +1714,10 @@ int lk_sync_counters_sum(uint64_t *sum) {
   if (rc) return rc;
   *sum = 0;
   GemmScratch &G = gemm_scratch();
-  if (!G.rsync) return LK_OK;
+  if (!G.tcnt) return LK_OK;
   HIP_TRY(hipDeviceSynchronize());
-  std::vector<unsigned> w((size_t)kRsyncRows * G.rsync_line * kChainLine);
-  HIP_TRY(hipMemcpy(w.data(), G.rsync, w.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+  std::vector<unsigned> w(G.tcnt_n);
+  HIP_TRY(hipMemcpy(w.data(), G.tcnt, w.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
   for (unsigned x : w) *sum += x;
   return LK_OK;
 }
@@ -1854,6 +1868,7 @@ struct lk_graph {
   // one host thread driving several devices (lk_comm_init_all): a sub-graph per device; this
   // graph only orchestrates (uploads to every part, levels in RCCL groups, outputs from part 0)
   std::vector<lk_graph *> parts;
+  bool broken = false;  // a compute failed inside an RCCL group: communicators aborted
   std::vector<Checked> c;
   std::vector<char> a_weight;
   std::vector<MirrorRef> pins;
@@ -2180,10 +2195,11 @@ int graph_compute_one(lk_graph *g) {
       (void)hipGetLastError();
     }
   }
+  const unsigned mark = fail_mark(g->device);
   if (g->exec) HIP_TRY(hipGraphLaunch(g->exec, st));
   else if ((rc = enqueue())) return rc;
   HIP_TRY(hipStreamSynchronize(st));
-  if ((rc = sync_failures(g->device))) return rc;  // nothing is written back from a failed launch
+  if ((rc = sync_failures(g->device, mark))) return rc;  // nothing is written back from a failed launch
   for (auto &x : g->d2h) std::memcpy(x.host, x.direct ? x.dev : g->staging + x.stage, x.bytes);
   g->computes++;
   return LK_OK;
@@ -2193,11 +2209,15 @@ int graph_compute_one(lk_graph *g) {
 // every part, each level of every part inside one RCCL group so the parts' all-gathers meet,
 // outputs read back from part 0, which like every part holds every gathered result).
 int graph_compute_parts(lk_graph *top) {
+  if (top->broken)
+    return fail(LK_ERR_DEVICE, "graph: unusable since a compute failed inside an RCCL group (communicators aborted)");
   int prev = 0;
   (void)hipGetDevice(&prev);
   int rc = LK_OK;
+  std::vector<unsigned> mark;
   for (auto *g : top->parts) {
     if ((rc = init_dev(g->device))) goto out;
+    mark.push_back(fail_mark(g->device));
     if (graph_stale(g)) {
       if ((rc = graph_bind(g, false))) goto out;
       g->rebinds++;
@@ -2217,7 +2237,14 @@ int graph_compute_parts(lk_graph *top) {
       if ((rc = init_dev(g->device)) || (rc = launch_level(g, l, S().devs[g->device].stream))) break;
     }
     const int re = lk_comm_group_end();
-    if (rc || (rc = re)) goto out;
+    if (rc || (rc = re)) {
+      // some parts enqueued their all-gathers and others did not: those collectives would wait for
+      // peers that never arrive. Abort every communicator (its enqueued work is torn down) and
+      // refuse further computes of this graph.
+      for (auto *g : top->parts) (void)lk_comm_abort(g->comm);
+      top->broken = true;
+      goto out;
+    }
   }
   {
     lk_graph *g0 = top->parts[0];
@@ -2233,8 +2260,8 @@ int graph_compute_parts(lk_graph *top) {
       rc = fail(LK_ERR_DEVICE, "graph: device %d failed", g->device);
       goto out;
     }
-  for (auto *g : top->parts)
-    if ((rc = sync_failures(g->device))) goto out;
+  for (size_t k = 0; k < top->parts.size(); k++)
+    if ((rc = sync_failures(top->parts[k]->device, mark[k]))) goto out;
   for (auto &x : top->parts[0]->d2h) std::memcpy(x.host, top->parts[0]->staging + x.stage, x.bytes);
   for (auto *g : top->parts) g->computes++;
 out:

@@ -294,20 +294,22 @@ static_assert(sizeof(StreamWork) == 64, "one s_load_dwordx16");
 
 constexpr int kChainLine = 32;  // chain sync words: one per 128-B line
 
-// Device-side waits (the fused split-K reductions, the chain plans' grid barriers) are bounded:
-// a wait that gives up counts itself in lk_sync_timeout_count (read and reset by lk_sync_timeouts)
-// and raises the host-visible word *lk_sync_fail_flag (page-locked host memory the library
-// installs per device), which every synchronous entry point checks after its sync and turns into
-// LK_ERR_DEVICE: a launch whose wait gave up never reports success. The bound is
-// lk_sync_wait_bound s_memrealtime ticks (100 MHz; 200 ms), changed only by lk_lab_set_sync_bound.
+// Device-side waits (only the opt-in chain plans' grid barriers since round 4: the split-K
+// reductions elect a last arriver and never wait) are bounded: a wait that gives up counts itself
+// in lk_sync_timeout_count (monotonic; lk_sync_timeouts reports the increase since its last call)
+// and stores the new count into the host-visible word *lk_sync_fail_flag (page-locked host memory
+// the library installs per device). Every synchronous entry point reads that word before its
+// launches and again after its sync, and a change becomes LK_ERR_DEVICE: a launch whose wait gave
+// up never reports success, whichever thread syncs first. The bound is lk_sync_wait_bound
+// s_memrealtime ticks (100 MHz; 200 ms), changed only by lk_set_sync_wait_bound.
 __device__ unsigned lk_sync_timeout_count;
 __device__ unsigned *lk_sync_fail_flag;
 __device__ uint64_t lk_sync_wait_bound = 20000000ull;
 
 __device__ __forceinline__ void lk_note_timeout() {
-  __hip_atomic_fetch_add(&lk_sync_timeout_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned n = __hip_atomic_fetch_add(&lk_sync_timeout_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   unsigned *f = lk_sync_fail_flag;
-  if (f) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (f) __hip_atomic_store(f, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 
@@ -1214,7 +1216,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_q_lds_kernel(GemmArgs g) {
     uint8_t *slot = smem + sl * G::STAGE;
 #pragma unroll
     for (int c = 0; c < G::C; c++) {
-      if (c < G::CA) dma16<2 == 2>(base_a, vofs[c], slot + ldso[c]);
+      if (c < G::CA) dma16<true>(base_a, vofs[c], slot + ldso[c]);
       else if (c < G::CA + G::CX) dma16<false>(base_x, vofs[c], slot + ldso[c]);
       else dma16<false>(base_t, vofs[c], slot + ldso[c]);
     }
@@ -1456,67 +1458,90 @@ __device__ __forceinline__ void skinny_blocks(const uint32_t (&w)[SB][WPB], cons
   }
 }
 
-// Fused split-K reduction (the skinny kernels, gemm_sk_kernel, gemm_wide_kernel): called by every wave of a
-// task once its partial slab rows [m0, m1) of slice `slice` are stored write-through (sc1) and
-// drained. One lane arrives on the row range's counter and waits until all `slices` tasks of the
-// range have arrived (the host launches every task co-resident: at most one workgroup per CU),
-// then the workgroup adds its 1/slices share of the range's rows, slabs in slice order — the
-// order of splitk_reduce_kernel, so the result is bit-identical to it.
-// Counters re-arm inside the launch: word 0 of the range's line counts arrivals, word 1
-// departures (a task departs once its wait is over); the last task to depart stores 0 to both,
-// when every task of the range is past its wait. So every launch starts from zeros (no counter
-// ever wraps), whatever the number of calls. One launch at a time per device uses a counter row.
-// Slab rows are N16 floats apart; the range covers columns [n_lo, n_lo + n_cnt) (n_cnt % 4 == 0).
-template <int NW>
-__device__ __forceinline__ void splitk_fused_reduce(unsigned *rsync, const __amdgpu_buffer_rsrc_t prs, int range, int slice,
-                                                    int slices, int m0, int m1, int M, int N, int N16, int n_lo, int n_cnt,
-                                                    uint8_t *dst, int64_t d_nb0, int64_t d_nb1, int wave, int lane) {
-  __builtin_amdgcn_s_barrier();
-  if (wave == 0 && lane == 0) {
-    unsigned *c = rsync + range * kChainLine;
-    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t ts = __builtin_amdgcn_s_memrealtime(), bound = lk_sync_wait_bound;
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)slices) {
-      if (__builtin_amdgcn_s_memrealtime() - ts >= bound) {  // not co-resident: flag it, run on
-        lk_note_timeout();
-        break;
+// Split-K fix-up by the last arriver (round 4; the skinny kernels, gemm_sk_kernel, gemm_wide_kernel).
+// Nobody waits for anybody: grids larger than the CUs that are free, and launches sharing the GPU
+// with other streams, are both safe. Per output tile (16 rows of a skinny kernel, one BM x BN tile of
+// the wide kernel) a counter word counts the slices whose partial slab rows are stored:
+//  * every slab is stored write-through (sc1) and the storing wave drains vmcnt(0) before it arrives;
+//  * one lane per tile adds 1 (agent-scope atomic); the add that returns slices − 1 is the last
+//    arrival: that lane re-arms the counter (stores 0: every slice has arrived, so no add is pending)
+//    and its workgroup sums the tile's slabs in slice order with sc1 loads — the order of
+//    splitk_reduce_kernel, so the result is bit-identical to it — into dst;
+//  * the other workgroups leave.
+// MI355X_MICROARCH.md (inter-workgroup visibility), hand-off row 1: sc1 stores and loads, the
+// signaller after its wave's vmcnt(0), "the workgroup whose add came last, told by the value its add
+// returned", its other waves loading after a workgroup barrier the adding wave joins.
+// Counters are per launch-tile and zero between launches (lk_sync_counters_sum); one batched launch
+// at a time per device owns them.
+__device__ __forceinline__ bool splitk_arrive(unsigned *cnt, unsigned slices) {
+  const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev + 1u != slices) return false;
+  __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// dst(m, n) = Σ_s slab_s(m, n) in slice order for item idx of a 4-column group: row m, columns
+// [n0, n0 + 4) (slab rows N16 floats apart, sc1 loads; all of a group's loads in flight at once).
+__device__ __forceinline__ void splitk_sum4(const __amdgpu_buffer_rsrc_t prs, int slices, int64_t m, int n0, int M, int N,
+                                            int N16, uint8_t *dst, int64_t d_nb0, int64_t d_nb1) {
+  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < slices; b += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      if (b + i < slices)
+        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)(b + i) * M + m) * N16 + n0) * 4), 0, 16));
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      if (b + i < slices) {
+        if (b + i == 0) sum = v[i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
+        else { sum.x += v[i].x; sum.y += v[i].y; sum.z += v[i].z; sum.w += v[i].w; }
       }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (__hip_atomic_fetch_add(c + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)slices - 1) {
-      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
-  asm volatile("" ::: "memory");  // the slab loads stay after the poll
-  __builtin_amdgcn_s_barrier();
-  const int per = (m1 - m0 + slices - 1) / slices;
-  const int r0 = min(m0 + slice * per, m1), r1 = min(r0 + per, m1);
-  const int c4 = n_cnt / 4;
-  for (int idx = (int)threadIdx.x; idx < (r1 - r0) * c4; idx += NW * 64) {
-    const int64_t m = r0 + idx / c4;
-    const int n0 = n_lo + (idx % c4) * 4;
-    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < slices; b += 8) {
-      f32x4 v[8];
+  const float e4[4] = {sum.x, sum.y, sum.z, sum.w};
+  if (d_nb0 == 4 && n0 + 4 <= N && (((uintptr_t)(dst + m * d_nb1 + n0 * 4)) & 15) == 0) {
+    *(f32x4 *)(dst + m * d_nb1 + n0 * 4) = sum;
+  } else {
 #pragma unroll
-      for (int i = 0; i < 8; i++)
-        if (b + i < slices)
-          v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)(b + i) * M + m) * N16 + n0) * 4), 0, 16));
-#pragma unroll
-      for (int i = 0; i < 8; i++)
-        if (b + i < slices) {
-          if (b + i == 0) sum = v[i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
-          else { sum.x += v[i].x; sum.y += v[i].y; sum.z += v[i].z; sum.w += v[i].w; }
-        }
+    for (int q = 0; q < 4; q++)
+      if (n0 + q < N) *(float *)(dst + m * d_nb1 + (n0 + q) * d_nb0) = e4[q];
+  }
+}
+
+// The skinny kernels' fix-up, called by every wave of the workgroup once its own stores have drained
+// (vmcnt(0)). Stream wave `sw` (or −1: a wave that stored nothing) stored the slab rows of its
+// `nunits` tiles t0 + sw + step·u; one instruction of that wave arrives on all of them at once (a lane
+// per tile, 64 per round), the last arrivals are listed in LDS (`lst`: a count per stream at
+// lst[sw], the tiles from lst[16 + sw·cap]), and after a workgroup barrier all NW·64 threads sum
+// the listed tiles' rows (16 rows x N16 columns each; rows past M skipped).
+template <int NW>
+__device__ __forceinline__ void splitk_tiles_fixup(unsigned *tcnt, const __amdgpu_buffer_rsrc_t prs, int slices, int sw,
+                                                   int nstreams, int t0, int step, int nunits, int cap, LK_LDS int *lst,
+                                                   int M, int N, int N16, uint8_t *dst, int64_t d_nb0, int64_t d_nb1,
+                                                   int lane) {
+  __syncthreads();  // every wave is past its loop (and long past its prologue reads of the list area)
+  if (sw >= 0) {
+    int n = 0;
+    for (int u0 = 0; u0 < nunits; u0 += 64) {
+      const int u = u0 + lane;
+      const int t = t0 + sw + step * u;
+      bool last = false;
+      if (u < nunits) last = splitk_arrive(tcnt + t, (unsigned)slices);
+      const uint64_t mask = __ballot(last);
+      if (last) lst[16 + sw * cap + n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] = t;
+      n += __builtin_popcountll(mask);
     }
-    const float e4[4] = {sum.x, sum.y, sum.z, sum.w};
-    if (d_nb0 == 4 && n0 + 4 <= N && (((uintptr_t)(dst + m * d_nb1 + n0 * 4)) & 15) == 0) {
-      *(f32x4 *)(dst + m * d_nb1 + n0 * 4) = sum;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (n0 + q < N) *(float *)(dst + m * d_nb1 + (n0 + q) * d_nb0) = e4[q];
+    if (lane == 0) lst[sw] = n;
+  }
+  asm volatile("" ::: "memory");  // the slab loads stay after the arrivals
+  __syncthreads();
+  const int c4 = N16 / 4;
+  for (int s = 0; s < nstreams; s++) {
+    const int n = lst[s];
+    for (int idx = (int)threadIdx.x; idx < n * 16 * c4; idx += NW * 64) {
+      const int t = lst[16 + s * cap + idx / (16 * c4)];
+      const int64_t m = (int64_t)t * 16 + (idx / c4) % 16;
+      if (m < M) splitk_sum4(prs, slices, m, (idx % c4) * 4, M, N, N16, dst, d_nb0, d_nb1);
     }
   }
 }
@@ -1684,9 +1709,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
     }
   }
   wait_vmcnt<0>();
-  if (g.rsync)
-    splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
-                            g.d_nb0, g.d_nb1, wave, lane);
+  if (g.rsync)  // the last slice to store a tile sums it (the staging area is free since the prologue)
+    splitk_tiles_fixup<NW>(g.rsync, prs, g.slices, wave, NW, t0, NW, nunits, (g.tiles_per_range + NW - 1) / NW,
+                           (LK_LDS int *)(LK_LDS void *)xlds, g.M, g.N, N16, g.dst, g.d_nb0, g.d_nb1, lane);
 }
 
 // ---- skinny GEMM on wave pairs (Q4_0 / Q4_1, 17 <= N <= 32) -------------------------------
@@ -2001,9 +2026,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     }
   }
   wait_vmcnt<0>();
-  if (g.rsync)
-    splitk_fused_reduce<NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
-                            g.d_nb0, g.d_nb1, wave, lane);
+  if (g.rsync)  // the last slice to store a tile sums it (the staging area is free since the prologue)
+    splitk_tiles_fixup<NW>(g.rsync, prs, g.slices, h == 0 ? p : -1, 4, t0, 4, nunits, (g.tiles_per_range + 3) / 4,
+                           (LK_LDS int *)(LK_LDS void *)xlds, g.M, g.N, N16, g.dst, g.d_nb0, g.d_nb1, lane);
 }
 
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------
@@ -2291,41 +2316,78 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
   const int npad = g.tiles_n * BN;
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * npad * 4 : 0, 0x00020000);
+  auto store_dst = [&](int64_t m, int n0, const f32x4 &v) __attribute__((always_inline)) {
+    const float e4[4] = {v.x, v.y, v.z, v.w};
+    if (g.d_nb0 == 4 && n0 + 4 <= g.N && ((((uintptr_t)g.dst + m * g.d_nb1 + n0 * 4) & 15) == 0)) {
+      *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = v;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+    }
+  };
   if (kg == 0) {
 #pragma unroll
-  for (int i = 0; i < MT; i++)
+    for (int i = 0; i < MT; i++)
 #pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const f32x4 o = red[(i * NT + j) * 64];
-      acc[i][j].x += o.x; acc[i][j].y += o.y; acc[i][j].z += o.z; acc[i][j].w += o.w;
-    }
-  // outputs: lane holds C'(n = 16·(tn·NT + j) + 4(lane>>4) + e, m = tm·BM + (mw·MT + i)·16 + (lane&15))
+      for (int j = 0; j < NT; j++) {
+        const f32x4 o = red[(i * NT + j) * 64];
+        acc[i][j].x += o.x; acc[i][j].y += o.y; acc[i][j].z += o.z; acc[i][j].w += o.w;
+      }
+    // outputs: lane holds C'(n = 16·(tn·NT + j) + 4(lane>>4) + e, m = tm·BM + (mw·MT + i)·16 + (lane&15))
 #pragma unroll
-  for (int i = 0; i < MT; i++) {
-    const int64_t m = (int64_t)tm * BM + (mw * MT + i) * 16 + (lane & 15);
-    if (m >= g.M) continue;
+    for (int i = 0; i < MT; i++) {
+      const int64_t m = (int64_t)tm * BM + (mw * MT + i) * 16 + (lane & 15);
+      if (m >= g.M) continue;
 #pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const int n0 = tn * BN + j * 16 + 4 * (lane >> 4);
-      if (g.slices > 1) {
-        store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * npad + n0, acc[i][j]);
-      } else {
-        const float e4[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
-        if (g.d_nb0 == 4 && n0 + 4 <= g.N && ((((uintptr_t)g.dst + m * g.d_nb1 + n0 * 4) & 15) == 0)) {
-          *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = acc[i][j];
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; q++)
-            if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
-        }
+      for (int j = 0; j < NT; j++) {
+        const int n0 = tn * BN + j * 16 + 4 * (lane >> 4);
+        if (g.slices > 1) store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * npad + n0, acc[i][j]);
+        else store_dst(m, n0, acc[i][j]);
       }
     }
   }
-  }
-  if (g.rsync) {  // every wave (both K-groups) joins: the tile's slices add up its rows
+  if (g.rsync) {
+    // split-K fix-up by the last arriver (splitk_arrive): the workgroup whose slice completes the
+    // tile sums it — its own slice from registers, the others' slabs by sc1 loads, in slice order
+    // (bit-identical to splitk_reduce_kernel); nobody waits for another workgroup
     wait_vmcnt<0>();
-    splitk_fused_reduce<8>(g.rsync, prs, tm * g.tiles_n + tn, slice, g.slices, tm * BM, min(tm * BM + BM, g.M), g.M, g.N, npad,
-                           tn * BN, BN, g.dst, g.d_nb0, g.d_nb1, wave, lane);
+    __syncthreads();
+    int *flag = (int *)smem;  // the ring is free (K-group 1's sums were read before this barrier)
+    if (threadIdx.x == 0) *flag = splitk_arrive(g.rsync + tm * g.tiles_n + tn, (unsigned)g.slices) ? 1 : 0;
+    __syncthreads();
+    asm volatile("" ::: "memory");
+    if (*flag && kg == 0) {
+      // per slab all MT·NT loads of the lane in flight at once (rows past M re-read row M − 1)
+      f32x4 sum[MT][NT];
+      for (int b = 0; b < g.slices; b++) {
+        f32x4 v[MT][NT];
+#pragma unroll
+        for (int i = 0; i < MT; i++) {
+          const int64_t m = min((int64_t)tm * BM + (mw * MT + i) * 16 + (lane & 15), (int64_t)g.M - 1);
+#pragma unroll
+          for (int j = 0; j < NT; j++) {
+            const int n0 = tn * BN + j * 16 + 4 * (lane >> 4);
+            v[i][j] = b == slice ? acc[i][j]
+                                 : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)b * g.M + m) * npad + n0) * 4), 0, 16));
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < MT; i++)
+#pragma unroll
+          for (int j = 0; j < NT; j++) {
+            if (b == 0) sum[i][j] = v[i][j];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
+            else { sum[i][j].x += v[i][j].x; sum[i][j].y += v[i][j].y; sum[i][j].z += v[i][j].z; sum[i][j].w += v[i][j].w; }
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < MT; i++) {
+        const int64_t m = (int64_t)tm * BM + (mw * MT + i) * 16 + (lane & 15);
+        if (m >= g.M) continue;
+#pragma unroll
+        for (int j = 0; j < NT; j++) store_dst(m, tn * BN + j * 16 + 4 * (lane >> 4), sum[i][j]);
+      }
+    }
   }
 }
 

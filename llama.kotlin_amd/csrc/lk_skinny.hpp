@@ -491,9 +491,9 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   }
   if (h == 0 && nunits > 0) collect(nunits - 1, prev);
   wait_vmcnt<0>();
-  if (g.rsync)
-    splitk_fused_reduce<G::NW>(g.rsync, prs, range, slice, g.slices, t0 * 16, min(t1 * 16, g.M), g.M, g.N, N16, 0, N16, g.dst,
-                               g.d_nb0, g.d_nb1, wave, lane);
+  if (g.rsync)  // the last slice to store a tile sums it (the fragment area is free since the prologue)
+    splitk_tiles_fixup<G::NW>(g.rsync, prs, g.slices, h == 0 ? p : -1, 4, t0, 4, nunits, (g.tiles_per_range + 3) / 4,
+                              (LK_LDS int *)xlds, g.M, g.N, N16, g.dst, g.d_nb0, g.d_nb1, lane);
 }
 
 

@@ -83,7 +83,7 @@ EXPORTED_SYMBOLS = (
     "lk_weights_cached_bytes", "lk_weights_cached_count",
     "lk_comm_unique_id", "lk_comm_init_rank", "lk_comm_init_all", "lk_comm_nranks", "lk_comm_rank",
     "lk_comm_device", "lk_comm_num_collectives",
-    "lk_comm_destroy", "lk_comm_group_start", "lk_comm_group_end",
+    "lk_comm_destroy", "lk_comm_abort", "lk_comm_group_start", "lk_comm_group_end",
     "lk_sharded_plan_create", "lk_sharded_plan_launch", "lk_sharded_plan_num_gathers", "lk_sharded_plan_destroy",
     "lk_dequantize_device", "lk_quantize_device", "lk_dot_direct", "lk_dot_direct_device",
     # include/lk_gguf.h
@@ -161,6 +161,8 @@ def load():
     L.lk_comm_num_collectives.restype = ctypes.c_uint64
     L.lk_comm_destroy.argtypes = [vp]
     L.lk_comm_destroy.restype = None
+    if hasattr(L, "lk_comm_abort"):  # (absent from round-3 lab builds loaded for A/B)
+        L.lk_comm_abort.argtypes = [vp]
     L.lk_sharded_plan_create.argtypes = [vp, P, P, P, ctypes.c_int, ctypes.POINTER(vp)]
     L.lk_sharded_plan_launch.argtypes = [vp, vp]
     L.lk_sharded_plan_num_gathers.argtypes = [vp]

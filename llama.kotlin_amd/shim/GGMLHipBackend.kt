@@ -134,23 +134,39 @@ fun computeDotProductQ80Q80Hip(graphAllocator: GGMLGraphAllocator, a: GGMLTensor
  * outside the run, or read by no node at all). Nodes the backend does not offload run one at a time
  * on GGMLCpuBackend between the runs.
  *
- * shards > 1: the GPUs 0 until shards of the node share every run — one RCCL communicator per GPU
- * (lk_comm_init_all), each run one lk_graph_create_sharded graph: rank r computes rows
- * [r·M/P, (r+1)·M/P) of every weight with only that shard pinned on its GPU, and an in-place
- * all-gather over xGMI per dependency level hands every GPU the whole result (SURVEY §8e).
+ * shards > 1 (default): every offloaded node runs as lk_mul_mat_sharded — shard r of its rows on
+ * GPU (device + r) mod lk_device_count(), results gathered through the host dst (the path the
+ * one-GPU boxes test; shards may exceed the GPU count).
+ * shards > 1 with rcclGraphs = true: the GPUs device, device + 1, … device + shards − 1 share every
+ * run — one RCCL communicator per GPU (lk_comm_init_all), each run one lk_graph_create_sharded
+ * graph: rank r computes rows [r·M/P, (r+1)·M/P) of every weight with only that shard pinned on its
+ * GPU, and an in-place all-gather over xGMI per dependency level hands every GPU the whole result
+ * (SURVEY §8e). This one-thread-drives-P-GPUs form has not run at P > 1 on hardware yet (the
+ * one-process-per-GPU form is what the bench's multi-GPU run uses); when fewer than `shards` GPUs
+ * are visible the backend falls back to the default form instead of failing.
  *
  * Residency contract: the host ByteArrays stay authoritative. Call bumpWeightGeneration()
  * whenever GGMLGraphAllocator re-places or rewrites tensor bytes (allocateGraph,
  * K/core/GGMLAlloc.kt:404-480) and evictBuffer(old) when reserve replaces a buffer (:392, :638).
  */
 class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1,
-                     private val wholeGraphs: Boolean = false) : GGMLBackend {
+                     private val wholeGraphs: Boolean = false,
+                     private val rcclGraphs: Boolean = false) : GGMLBackend {
     private val cpu = GGMLCpuBackend()
 
-    /** shards > 1: rank r's communicator on GPU r (lk_comm_init_all), shared by every sharded run. */
+    /** rcclGraphs and shards > 1 with that many GPUs from `device` on: rank r's communicator on GPU
+     *  device + r (lk_comm_init_all), shared by every sharded run; null otherwise. */
     private val comms: CPointer<CPointerVar<lk_comm>>? =
-        if (shards > 1) nativeHeap.allocArray<CPointerVar<lk_comm>>(shards).also { arr ->
-            checkStatus(lk_comm_init_all(shards, null, arr))
+        if (rcclGraphs && shards > 1 && device + shards <= lk_device_count()) {
+            val arr = nativeHeap.allocArray<CPointerVar<lk_comm>>(shards)
+            memScoped {
+                val devs = allocArray<IntVar>(shards)
+                for (r in 0 until shards) devs[r] = device + r
+                val st = lk_comm_init_all(shards, devs, arr)
+                if (st != LK_OK.toInt()) nativeHeap.free(arr)
+                checkStatus(st)  // a constructor that cannot build its communicators throws
+            }
+            arr
         } else null
 
     /** The generation cached weight mirrors are current for (lk_weights_pin semantics). */
@@ -240,7 +256,15 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1,
                 }
                 var j = i
                 while (j < nodes.size && supportsOp(nodes[j])) j++
-                computeRun(ga, nodes, i, j)  // one lk_graph (row-sharded over the GPUs when shards > 1)
+                if (shards > 1 && comms == null) {
+                    // row shards node by node through the host dst (lk_mul_mat_sharded)
+                    for (k in i until j) {
+                        val n = nodes[k]
+                        computeMatMulHip(ga, GGMLContext(), n.src[0]!!, n.src[1]!!, n, weightGeneration, shards)
+                    }
+                } else {
+                    computeRun(ga, nodes, i, j)  // one lk_graph (row-sharded over the GPUs with comms)
+                }
                 i = j
             }
             GGMLStatus.SUCCESS

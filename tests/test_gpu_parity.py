@@ -293,7 +293,7 @@ def test_backend_graph_compute(gpu, oracle):
 
 
 @pytest.mark.parametrize("qt,M,K", [(6, 4096, 4096), (2, 11008, 4096), (2, 4096, 11008), (3, 11008, 4096),
-                                    (2, 4096, 4096)])
+                                    (3, 4096, 11008), (2, 4096, 4096)])
 def test_full_size_batch1_vs_oracle(gpu, oracle, qt, M, K):
     """BASELINE configs C2/C3 and the Q4_0 4096^2 headline shape at full size, N = 1."""
     q, x = make_inputs(oracle, qt, M, K, 1, seed=M + K)
@@ -304,7 +304,7 @@ def test_full_size_batch1_vs_oracle(gpu, oracle, qt, M, K):
 
 
 @pytest.mark.parametrize("qt,M,K,N", [(2, 11008, 4096, 32), (3, 11008, 4096, 32), (2, 4096, 11008, 32),
-                                      (6, 4096, 4096, 32)])
+                                      (3, 4096, 11008, 32), (6, 4096, 4096, 32)])
 def test_full_size_batched_vs_oracle(gpu, oracle, qt, M, K, N):
     """BASELINE config C3 at batch 32 (and Q8_0 4096^2 at batch 32), full size."""
     q, x = make_inputs(oracle, qt, M, K, N, seed=M + K + N)

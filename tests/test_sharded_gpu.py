@@ -235,3 +235,43 @@ def test_rccl_sharded_graph_equals_graph(gpu, oracle, mode):
     g.close(); plain.close()
     for c in comms:
         c.close()
+
+
+def test_comm_from_world1_nccl_process_group(gpu, oracle):
+    """The bench's N > 1 set-up at world size 1: a torch.distributed NCCL (= RCCL) process group,
+    Comm.from_process_group (rank 0's unique id broadcast through the group, lk_comm_init_rank on
+    the current device), then a Llama-shape sharded plan captured in a HIP graph — bit-equal to
+    lk_plan over the same nodes."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    import ggml_hip as G
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        comm = G.Comm.from_process_group()
+        assert comm.nranks == 1 and comm.rank == 0 and comm.device == dev.index
+        ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 26)
+        nodes = _llama_nodes(G, ga, oracle, [(4096, 4096), (11008, 4096)], seed=5)
+        refs = [ga.allocateTensor(G.GGMLType.F32, [1, d.ne[1]]) for (_, _, d) in nodes]
+        plan = G.ShardedMulMatPlan(comm, ga, [(G.shard_view(a, 1, 0), x, d) for (a, x, d) in nodes])
+        ref = G.MulMatPlan(ga, [(a, x, r) for (a, x, _), r in zip(nodes, refs)])
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            ref.launch(stream=s)
+        torch.cuda.synchronize()
+        hg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(hg, stream=s):
+            plan.launch(stream=s)
+        for _ in range(2):
+            hg.replay()
+        torch.cuda.synchronize()
+        for (_, _, d), r in zip(nodes, refs):
+            assert bytes(ga.tensorBytes(d).cpu().numpy()) == bytes(ga.tensorBytes(r).cpu().numpy())
+        del hg
+        plan.close(); comm.close()
+    finally:
+        dist.destroy_process_group()
