@@ -191,21 +191,24 @@ int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor
  * then undefined) and re-arms the plan; 0 otherwise. Synchronizes the device. */
 int lk_plan_chain_timed_out(lk_plan *plan);
 void lk_plan_destroy(lk_plan *plan);
-/* Batched MUL_MATs (2 <= N) reduce their K slices inside the launch, workgroups waiting for each
- * other (every workgroup co-resident: at most one per CU), and chain plans wait at grid barriers.
- * Every such wait is bounded (200 ms). A wait that gives up raises a per-device flag: the next
- * synchronous entry point on that device (lk_mul_mat, lk_mul_mat_sharded, lk_graph_compute)
- * returns LK_ERR_DEVICE instead of LK_OK — those results are undefined (GGMLStatus.FAILED at
- * backend level, core/GGMLCpuBackend.kt:167-176). Stream-ordered entry points (lk_mul_mat_device,
- * lk_plan_launch) cannot report it at launch; a caller of those reads it here:
- * *count = how many waits on the current device gave up since the last call; the count and the
- * flag are then reset. Synchronizes the device. Diagnostic; no reference counterpart. */
+/* Batched MUL_MATs (2 <= N) split K over workgroups and sum the slices inside the launch by the
+ * LAST ARRIVER per output tile (round 4): nobody waits for another workgroup, so any grid size and
+ * kernels of other streams sharing the GPU are safe. Only chain plans still wait (grid barriers,
+ * every workgroup resident: one per CU). Such a wait is bounded (200 ms); one that gives up is
+ * counted on the device and moves a per-device failure word: every synchronous entry point
+ * (lk_mul_mat, lk_mul_mat_sharded, lk_graph_compute) reads the word before its launches and again
+ * after its sync and returns LK_ERR_DEVICE when it moved — those results are undefined
+ * (GGMLStatus.FAILED at backend level, core/GGMLCpuBackend.kt:167-176). Stream-ordered entry points
+ * (lk_mul_mat_device, lk_plan_launch) cannot report it at launch; a caller of chain plans reads
+ * lk_plan_chain_timed_out, or here: *count = how many waits on the current device gave up since
+ * the last call (the device count is monotonic). Synchronizes the device. Diagnostic; no reference
+ * counterpart. */
 int lk_sync_timeouts(uint32_t *count);
 /* Test hooks of the same mechanism (current device; synchronize it first):
  * lk_set_sync_wait_bound — the wait bound in 100 MHz ticks (default 20000000 = 200 ms); 0 makes a
  *   waiter that does not find its peers already arrived give up at once (tests of the error path);
- * lk_sync_counters_sum — the sum of every split-K arrival/departure counter word, 0 between
- *   launches (the counters re-arm inside each launch). */
+ * lk_sync_counters_sum — the sum of every split-K per-tile arrival counter word, 0 between
+ *   launches (the last arrival of each tile re-arms its word). */
 int lk_set_sync_wait_bound(uint64_t ticks);
 int lk_sync_counters_sum(uint64_t *sum);
 

@@ -24,6 +24,7 @@
 
 #include "lk_kernels.hpp"
 #include "lk_skinny.hpp"
+#include "lk_kpart.hpp"
 #include "../../include/lk_gguf.h"
 
 using namespace lk;
@@ -402,8 +403,8 @@ int splitk_counters(int slices, size_t slab_bytes, int64_t ntiles, bool list_ok,
   *out = nullptr;
   if (unfused || slices <= 1 || !list_ok || slab_bytes >= (1ull << 31) || ntiles <= 0) return LK_OK;
   GemmScratch &S = gemm_scratch();
-  if (S.tcnt_n < (size_t)ntiles) {
-    const size_t want = std::max<size_t>((size_t)ntiles, 1 << 14);
+  if (S.tcnt_n < (size_t)ntiles * kChainLine) {  // a 128-B line per tile
+    const size_t want = std::max<size_t>((size_t)ntiles * kChainLine, 1 << 16);
     if (S.tcnt) HIP_TRY(hipFree(S.tcnt));
     S.tcnt = nullptr;
     S.tcnt_n = 0;
@@ -567,7 +568,7 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
-  const bool list_ok = 16 + SG::NW * ((g.tiles_per_range + SG::NW - 1) / SG::NW) <= SG::XB / 4;
+  const bool list_ok = 1 + (g.tiles_per_range + SG::NW - 1) / SG::NW <= SG::D * SG::SLOT / 4;  // a wave's ring
   if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, &rsync)) return rf;
   g.slices = slices;
   if (slices > 1) {
@@ -603,7 +604,7 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
-  const bool list_ok = 16 + 4 * ((g.tiles_per_range + 3) / 4) <= SG::XB / 4;
+  const bool list_ok = 1 + (g.tiles_per_range + 3) / 4 <= NT * 64 * 4;  // parity 0 of a pair's hand-off
   if (int rc = splitk_counters(slices, slab_bytes, ntile, list_ok, &rsync)) return rc;
   const bool fuse = rsync != nullptr;
   g.slices = slices;
@@ -658,7 +659,7 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
-  const bool list_ok = 16 + 4 * ((g.tiles_per_range + 3) / 4) <= SG::XF / 4;
+  const bool list_ok = 1 + (g.tiles_per_range + 3) / 4 <= NT * 64 * 4;  // parity 0 of a pair's hand-off
   if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, &rsync)) return rf;
   g.slices = slices;
   if (slices > 1) {
@@ -682,7 +683,61 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   return LK_OK;
 }
 
+bool getenv_flag(const char *name);
+
+// gemm_kpart_kernel (lk_kpart.hpp): Q4_0 / Q4_1 at 2 <= N <= 32, K split over the waves of a
+// workgroup (8·KB blocks per workgroup) and over slices of that span; per-tile sums in LDS, the
+// slices' slabs summed by the last arriver. One workgroup per CU (LDS); grids may exceed the CUs.
+template <int QT, int NT>
+int launch_kpart_t(const SkinnyArgs &s, hipStream_t st) {
+  using KG = KpartGeom<QT, NT>;
+  GemmScratch &S = gemm_scratch();
+  // the activation fragments (xsplit_kernel) in the k order of QT's code decode, and T per (block,
+  // column): Q4_0 −136·Σ(hi + lo) (codes 128 + n), Q4_1 Σx (codes n·2⁻⁹)
+  const int64_t nblk = s.K / 32, ntx = (s.N + 15) / 16;
+  const size_t fb = (size_t)ntx * nblk * kXSplits * 64 * 16, sb = (size_t)nblk * ntx * 16 * sizeof(float);
+  if (int rc = grow(&S.frag, &S.frag_bytes, fb + sb)) return rc;
+  XSplitArgs xa{};
+  xa.b = s.b;
+  xa.b_nb0 = s.b_nb0; xa.b_nb1 = s.b_nb1;
+  xa.N = s.N; xa.K = s.K;
+  xa.frag = (u32x4 *)S.frag;
+  xa.xsum = (float *)((uint8_t *)S.frag + fb);
+  xa.mult = QT == LK_TYPE_Q4_0 ? -136.f : 1.f;
+  xa.q4_order = QT == LK_TYPE_Q4_0 ? 2 : 1;
+  KpartArgs g{};
+  g.a = s.a; g.frag = xa.frag; g.xsum = xa.xsum;
+  g.dst = s.dst; g.d_nb0 = s.d_nb0; g.d_nb1 = s.d_nb1;
+  g.M = s.M; g.N = s.N; g.K = s.K;
+  const int slices = (int)((nblk + KG::SPAN - 1) / KG::SPAN);
+  const int ntile = (g.M + 15) / 16;
+  // one workgroup per CU (LDS); at most 64 tiles per range (the per-wave fix-up's lane mask)
+  int ranges = std::max({1, std::min(ntile, cu_count() / slices), (ntile + 63) / 64});
+  const int tpr = (ntile + ranges - 1) / ranges;
+  ranges = (ntile + tpr - 1) / tpr;
+  g.tiles_per_range = tpr;
+  g.slices = slices;
+  if (slices > 1) {
+    const size_t slab_bytes = (size_t)slices * g.M * 16 * NT * sizeof(float);
+    if (int rc = grow(&S.partial, &S.partial_bytes, slab_bytes)) return rc;
+    g.partial = (float *)S.partial;
+    if (int rc = splitk_counters(slices, slab_bytes, ntile, true, &g.tcnt)) return rc;
+  }
+  g.tasks = ranges * slices;
+  launch_xsplit(xa, st);
+  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  hipLaunchKernelGGL((gemm_kpart_kernel<QT, NT>), dim3(grid), dim3(KG::NW * 64), KG::LDS, st, g);
+  if (slices > 1 && !g.tcnt) {
+    const int64_t threads = (int64_t)g.M * (16 * NT / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
+                       slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);
+  }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
 int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  static const bool no_kpart = getenv_flag("LK_KPART_OFF");  // A/B: the round-3 skinny / pair kernels
   SkinnyArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
   g.b = (const uint8_t *)b->data + b->data_offset;
@@ -690,8 +745,10 @@ int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   g.dst = (uint8_t *)dst->data + dst->data_offset;
   g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
-  // Q4_0 / Q4_1 at 17 <= N <= 32 on wave pairs (gemm_skinny_pair_kernel), the rest one wave per stream
+  // Q4_0 / Q4_1 on the K-partitioned kernel (round 4); Q8_0 one wave per stream
   const bool one = c.N <= 16;
+  if (!no_kpart && a->type == LK_TYPE_Q4_0) return one ? launch_kpart_t<LK_TYPE_Q4_0, 1>(g, st) : launch_kpart_t<LK_TYPE_Q4_0, 2>(g, st);
+  if (!no_kpart && a->type == LK_TYPE_Q4_1) return one ? launch_kpart_t<LK_TYPE_Q4_1, 1>(g, st) : launch_kpart_t<LK_TYPE_Q4_1, 2>(g, st);
   switch (a->type) {
     case LK_TYPE_Q4_0: return one ? launch_skinny_t<LK_TYPE_Q4_0, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_0, 2>(g, st);
     case LK_TYPE_Q4_1: return one ? launch_skinny_t<LK_TYPE_Q4_1, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_1, 2>(g, st);
@@ -2466,3 +2523,14 @@ int lk_dot_direct(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t 
   HIP_TRY(hipStreamSynchronize(st));
   return LK_OK;
 }
+
+#ifdef LK_LAB_STAMPS
+// lab builds only (tools/stamp_kpart.py): the gemm_kpart_kernel timeline stamps
+extern "C" int lk_lab_stamps(uint64_t *out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(lk::lk_kp_stamps), sizeof(uint64_t) * (size_t)std::min(n, 1024 * 8 * 10)) == hipSuccess ? 0 : 5;
+}
+extern "C" int lk_lab_stamps_clear(void) {
+  static uint64_t zero[1024 * 8 * 10];
+  return hipMemcpyToSymbol(HIP_SYMBOL(lk::lk_kp_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : 5;
+}
+#endif

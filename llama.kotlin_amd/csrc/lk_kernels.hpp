@@ -1458,6 +1458,18 @@ __device__ __forceinline__ void skinny_blocks(const uint32_t (&w)[SB][WPB], cons
   }
 }
 
+// Lab timelines (built only with -DLK_LAB_STAMPS by tools/build_lab.sh, never in the product
+// library): per (workgroup, wave) s_memrealtime stamps and per-wave sums, read by lk_lab_stamps
+// (lk_hip.hip) into tools/stamp_kpart.py. Slot meanings are the kernel's (see its LK_KP_SET calls).
+#ifdef LK_LAB_STAMPS
+__device__ uint64_t lk_kp_stamps[1024][8][10];
+#define LK_KP_T() __builtin_amdgcn_s_memrealtime()
+#define LK_KP_SET(i, v) do { if (lane == 0 && blockIdx.x < 1024) lk_kp_stamps[blockIdx.x][wave][i] = (v); } while (0)
+#else
+#define LK_KP_T() 0ull
+#define LK_KP_SET(i, v) do { } while (0)
+#endif
+
 // Split-K fix-up by the last arriver (round 4; the skinny kernels, gemm_sk_kernel, gemm_wide_kernel).
 // Nobody waits for anybody: grids larger than the CUs that are free, and launches sharing the GPU
 // with other streams, are both safe. Per output tile (16 rows of a skinny kernel, one BM x BN tile of
@@ -1471,8 +1483,9 @@ __device__ __forceinline__ void skinny_blocks(const uint32_t (&w)[SB][WPB], cons
 // MI355X_MICROARCH.md (inter-workgroup visibility), hand-off row 1: sc1 stores and loads, the
 // signaller after its wave's vmcnt(0), "the workgroup whose add came last, told by the value its add
 // returned", its other waves loading after a workgroup barrier the adding wave joins.
-// Counters are per launch-tile and zero between launches (lk_sync_counters_sum); one batched launch
-// at a time per device owns them.
+// Counters are per launch-tile, each on a 128-B line of its own (kChainLine words apart: returning
+// atomics on one line serialize at the memory side, ~12 ns each), and zero between launches
+// (lk_sync_counters_sum); one batched launch at a time per device owns them.
 __device__ __forceinline__ bool splitk_arrive(unsigned *cnt, unsigned slices) {
   const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (prev + 1u != slices) return false;
@@ -1510,38 +1523,95 @@ __device__ __forceinline__ void splitk_sum4(const __amdgpu_buffer_rsrc_t prs, in
 
 // The skinny kernels' fix-up, called by every wave of the workgroup once its own stores have drained
 // (vmcnt(0)). Stream wave `sw` (or −1: a wave that stored nothing) stored the slab rows of its
-// `nunits` tiles t0 + sw + step·u; one instruction of that wave arrives on all of them at once (a lane
-// per tile, 64 per round), the last arrivals are listed in LDS (`lst`: a count per stream at
-// lst[sw], the tiles from lst[16 + sw·cap]), and after a workgroup barrier all NW·64 threads sum
-// the listed tiles' rows (16 rows x N16 columns each; rows past M skipped).
-template <int NW>
+// `nunits` tiles t0 + sw + step·u. It arrives on all of them at once, as soon as its own loop is done
+// (one instruction: a lane per tile, 64 per round) — no workgroup barrier first, so for each tile the
+// last arrival is the slowest of the slices' streams for THAT tile, and the summing spreads over the
+// range's workgroups instead of landing on the slowest one. Its last arrivals go to its own LDS list
+// (`lst`: the count at lst[0], the tiles from lst[1]; an area only this wave uses by now), then after
+// one workgroup barrier all NW·64 threads sum the listed tiles of every stream (lists at lst_of(s)),
+// 16 rows x N16 columns each (rows past M skipped), with the loads of 4 items per thread in flight.
+template <int NW, typename ListOf>
 __device__ __forceinline__ void splitk_tiles_fixup(unsigned *tcnt, const __amdgpu_buffer_rsrc_t prs, int slices, int sw,
-                                                   int nstreams, int t0, int step, int nunits, int cap, LK_LDS int *lst,
+                                                   int nstreams, int t0, int step, int nunits, ListOf lst_of,
                                                    int M, int N, int N16, uint8_t *dst, int64_t d_nb0, int64_t d_nb1,
                                                    int lane) {
-  __syncthreads();  // every wave is past its loop (and long past its prologue reads of the list area)
   if (sw >= 0) {
+    LK_LDS int *lst = lst_of(sw);
     int n = 0;
     for (int u0 = 0; u0 < nunits; u0 += 64) {
       const int u = u0 + lane;
       const int t = t0 + sw + step * u;
       bool last = false;
-      if (u < nunits) last = splitk_arrive(tcnt + t, (unsigned)slices);
+      if (u < nunits) last = splitk_arrive(tcnt + (int64_t)t * kChainLine, (unsigned)slices);
       const uint64_t mask = __ballot(last);
-      if (last) lst[16 + sw * cap + n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] = t;
+      if (last) lst[1 + n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] = t;
       n += __builtin_popcountll(mask);
     }
-    if (lane == 0) lst[sw] = n;
+    if (lane == 0) lst[0] = n;
   }
   asm volatile("" ::: "memory");  // the slab loads stay after the arrivals
+#ifdef LK_LAB_STAMPS
+  const int wave = threadIdx.x >> 6;
+  LK_KP_SET(5, LK_KP_T());
+#endif
   __syncthreads();
-  const int c4 = N16 / 4;
-  for (int s = 0; s < nstreams; s++) {
-    const int n = lst[s];
-    for (int idx = (int)threadIdx.x; idx < n * 16 * c4; idx += NW * 64) {
-      const int t = lst[16 + s * cap + idx / (16 * c4)];
-      const int64_t m = (int64_t)t * 16 + (idx / c4) % 16;
-      if (m < M) splitk_sum4(prs, slices, m, (idx % c4) * 4, M, N, N16, dst, d_nb0, d_nb1);
+#ifdef LK_LAB_STAMPS
+  LK_KP_SET(6, LK_KP_T());
+  if (sw >= 0) LK_KP_SET(7, (uint64_t)lst_of(sw)[0]);
+#endif
+  const int c4 = N16 / 4, per = 16 * c4;
+  int tot = 0;
+  for (int s = 0; s < nstreams; s++) tot += lst_of(s)[0] * per;
+  // item i: stream list by list, tile by tile, row by row, 4 columns
+  auto item = [&](int i, int64_t &m, int &n0) __attribute__((always_inline)) {
+    int s = 0, k = i;
+    while (k >= lst_of(s)[0] * per) { k -= lst_of(s)[0] * per; s++; }
+    const int t = lst_of(s)[1 + k / per];
+    m = (int64_t)t * 16 + (k % per) / c4;
+    n0 = (k % c4) * 4;
+  };
+  constexpr int IB = 4;  // items per thread with their loads in flight together
+  for (int i0 = (int)threadIdx.x * IB; i0 < tot; i0 += NW * 64 * IB) {
+    int64_t m[IB];
+    int n0[IB];
+    bool ok[IB];
+#pragma unroll
+    for (int q = 0; q < IB; q++) {
+      ok[q] = i0 + q < tot;
+      m[q] = 0; n0[q] = 0;
+      if (ok[q]) item(i0 + q, m[q], n0[q]);
+      ok[q] = ok[q] && m[q] < M;
+    }
+    f32x4 sum[IB];
+    for (int b = 0; b < slices; b += 8) {
+      f32x4 v[IB][8];
+#pragma unroll
+      for (int q = 0; q < IB; q++)
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if (ok[q] && b + i < slices)
+            v[q][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)(b + i) * M + m[q]) * N16 + n0[q]) * 4), 0, 16));
+#pragma unroll
+      for (int q = 0; q < IB; q++)
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if (ok[q] && b + i < slices) {
+            if (b + i == 0) sum[q] = v[q][i];  // slab 0 as is (0 + x would turn -0.0 into +0.0)
+            else { sum[q].x += v[q][i].x; sum[q].y += v[q][i].y; sum[q].z += v[q][i].z; sum[q].w += v[q][i].w; }
+          }
+    }
+#pragma unroll
+    for (int q = 0; q < IB; q++) {
+      if (!ok[q]) continue;
+      const float e4[4] = {sum[q].x, sum[q].y, sum[q].z, sum[q].w};
+      uint8_t *o = dst + m[q] * d_nb1 + n0[q] * d_nb0;
+      if (d_nb0 == 4 && n0[q] + 4 <= N && (((uintptr_t)o) & 15) == 0) {
+        *(f32x4 *)o = sum[q];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+          if (n0[q] + e < N) *(float *)(dst + m[q] * d_nb1 + (n0[q] + e) * d_nb0) = e4[e];
+      }
     }
   }
 }
@@ -1709,9 +1779,13 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
     }
   }
   wait_vmcnt<0>();
-  if (g.rsync)  // the last slice to store a tile sums it (the staging area is free since the prologue)
-    splitk_tiles_fixup<NW>(g.rsync, prs, g.slices, wave, NW, t0, NW, nunits, (g.tiles_per_range + NW - 1) / NW,
-                           (LK_LDS int *)(LK_LDS void *)xlds, g.M, g.N, N16, g.dst, g.d_nb0, g.d_nb1, lane);
+  if (g.rsync) {  // the last slice to store a tile sums it; wave w lists in its own ring, drained by now
+    auto lst_of = [&](int w) __attribute__((always_inline)) {
+      return (LK_LDS int *)(LK_LDS void *)(smem + G::XB + G::TB + w * D * G::SLOT);
+    };
+    splitk_tiles_fixup<NW>(g.rsync, prs, g.slices, wave, NW, t0, NW, nunits, lst_of, g.M, g.N, N16, g.dst, g.d_nb0,
+                           g.d_nb1, lane);
+  }
 }
 
 // ---- skinny GEMM on wave pairs (Q4_0 / Q4_1, 17 <= N <= 32) -------------------------------
@@ -1836,6 +1910,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   // XCD-aware task order, as gemm_skinny_kernel
   const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
   if (task >= g.tasks) return;  // grid padding (before any barrier: the whole workgroup leaves)
+  [[maybe_unused]] const uint64_t t_entry = LK_KP_T();
   if (threadIdx.x < 16) flags[threadIdx.x] = 0;  // published by the prologue's barrier
   const int slice = task % g.slices, range = task / g.slices;
   const int nblk = g.K / 32;
@@ -1956,6 +2031,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
   const int SH = h == 0 ? NT : 0;  // stores per unit (at least; slices == 1 may store more)
+  [[maybe_unused]] const uint64_t t_loop = LK_KP_T();
   for (int u = 0; u < nunits; u++) {
     // the pair's two waves take turns at issue priority, one unit each, h = 1 (the younger) first
     // (A/B, three rounds: C3 Q4_0 21.2 -> 20.7 us, Q4_1 21.1 -> 20.7 us)
@@ -2026,9 +2102,17 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     }
   }
   wait_vmcnt<0>();
-  if (g.rsync)  // the last slice to store a tile sums it (the staging area is free since the prologue)
-    splitk_tiles_fixup<NW>(g.rsync, prs, g.slices, h == 0 ? p : -1, 4, t0, 4, nunits, (g.tiles_per_range + 3) / 4,
-                           (LK_LDS int *)(LK_LDS void *)xlds, g.M, g.N, N16, g.dst, g.d_nb0, g.d_nb1, lane);
+  [[maybe_unused]] const uint64_t t_end = LK_KP_T();
+  if (g.rsync) {  // the last slice to store a tile sums it; stream p lists in its pair's hand-off area
+    // (parity 0 of pair p: both of the pair's waves are past their last hand-off by now)
+    auto lst_of = [&](int s) __attribute__((always_inline)) {
+      return (LK_LDS int *)(LK_LDS void *)(smem + G::XB + G::TB + s * NT * 64 * 16);
+    };
+    splitk_tiles_fixup<NW>(g.rsync, prs, g.slices, h == 0 ? p : -1, 4, t0, 4, nunits, lst_of, g.M, g.N, N16, g.dst,
+                           g.d_nb0, g.d_nb1, lane);
+  }
+  LK_KP_SET(0, t_entry); LK_KP_SET(2, t_loop); LK_KP_SET(3, t_end); LK_KP_SET(4, LK_KP_T());
+  LK_KP_SET(8, (uint64_t)nunits);
 }
 
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------
@@ -2354,7 +2438,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
     wait_vmcnt<0>();
     __syncthreads();
     int *flag = (int *)smem;  // the ring is free (K-group 1's sums were read before this barrier)
-    if (threadIdx.x == 0) *flag = splitk_arrive(g.rsync + tm * g.tiles_n + tn, (unsigned)g.slices) ? 1 : 0;
+    if (threadIdx.x == 0) *flag = splitk_arrive(g.rsync + (int64_t)(tm * g.tiles_n + tn) * kChainLine, (unsigned)g.slices) ? 1 : 0;
     __syncthreads();
     asm volatile("" ::: "memory");
     if (*flag && kg == 0) {

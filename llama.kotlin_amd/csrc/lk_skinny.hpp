@@ -1,29 +1,28 @@
-// lk_skinny.hpp — Q4_0 / Q4_1 x F32 at 2 <= N <= 32 (config C3's batch 32) on gfx950.
+// lk_skinny.hpp — gemm_sk_kernel: Q4_K x F32 at 16 <= N <= 32 on gfx950 (wave-pair MFMA).
 //
-// computeMatMul's quantized dots (core/GGMLComputeOps.kt:70-145, dispatched at :1448-1480) for
-// a few activation columns, on v_mfma_f32_16x16x32_bf16. Arithmetic:
+// computeMatMul's Q4_K branch (core/GGMLComputeOps.kt:1483-1514, dot :241-310) for a few
+// activation columns, on v_mfma_f32_16x16x32_bf16. Since round 3 the kernel is instantiated for
+// Q4_K only (Q4_0 / Q4_1 run on gemm_skinny_pair_kernel, lk_kernels.hpp, which was faster for
+// them). Arithmetic:
 //
-//  * Activations as bf16 hi + lo (|x − hi − lo| ≤ 2⁻¹⁷|x|), split once per call by xsplit_kernel
-//    into 1-KB MFMA operand fragments, plus S = Σx per (block, column).
-//  * Codes as the exact bf16 128 + n, two per v_and_or_b32: (u & 0x000F000F) | 0x43004300 (bf16
-//    0x43 0x0n = 128 + n), so a lane's 8 codes cost 7 VALU (k order 0,4,1,5,2,6,3,7, which
-//    xsplit writes the activations in). The MFMA gives p = Σ (128 + n)·x per block.
-//  * Per block: acc += d·p (packed f32 FMAs). The offsets fold into one f32 term per block,
-//    e·S with e = −136·d (Q4_0: d·(n − 8) = d·(128 + n) − 136·d) or e = m − 128·d (Q4_1:
-//    d·n + m), summed over a wave's 8 blocks by two v_mfma_f32_16x16x4_f32 per 16-column tile
-//    (exact f32 products) straight into the accumulators.
+//  * Activations as bf16 hi + lo (|x − hi − lo| ≤ 2⁻¹⁷|x|), in MFMA operand fragments, plus
+//    S = Σ(hi + lo) per (sub-block, column). Dense 16-byte-aligned activations (fx) are split by
+//    the kernel itself: the slice's raw rows land in LDS by LDS-DMA and each wave splits its items
+//    in place; other layouts come from xsplit_kernel (one extra launch).
+//  * Codes as the exact bf16 128 + n, two per v_and_or_b32: (u & 0x000F000F) | 0x43004300, k order
+//    0,4,1,5,2,6,3,7 (the order the split writes the activations in). The MFMA gives
+//    p = Σ (128 + n)·x per 32-weight sub-block.
+//  * Per sub-block: acc += s1·p (packed f32 FMAs), s1 = qs·d/945 — the affine form q·s1 + min of
+//    the Kotlin (q/15)·scale + min. The offsets fold into one f32 term per sub-block,
+//    e·S with e = min − 128·s1, summed over a wave's 8 sub-blocks by two v_mfma_f32_16x16x4_f32
+//    per 16-column tile (exact f32 products) straight into the accumulators.
 //
-// On gfx950 a SIMD issues one wave64 VALU instruction per ~4.3 cycles whether one or two waves
-// share it (round-2 lab tool valu_rate.hip, removed), so the VALU count per block, not latency, sets the pace:
-// 8 + 1 + NT·2 VALU per block here against ~25 for the fp8-conversion decode with scalar FMAs.
-//
-// Schedule: workgroup = (row range, K slice of 16 blocks), 8 waves; wave (stream p = w % 4,
-// half h = w / 4) streams 16-row tiles t0 + p + 4i, its half's eight blocks of each row through
-// its own LDS-DMA ring. The slice's fragments and block sums are landed in LDS once by LDS-DMA
-// and read into VGPRs (each wave: its 8 blocks). The h = 1 wave (issue priority 1) hands its
-// accumulators to its partner through LDS (ready / ack flags, 2 parities); the h = 0 wave adds
-// them one unit later, in a fixed order, and stores (partial slab per slice, reduced in slice
-// order: deterministic).
+// Schedule: workgroup = (row range, K slice of 16 sub-blocks = two Q4_K blocks), 8 waves; wave
+// (stream p = w % 4, half h = w / 4) streams 16-row tiles t0 + p + 4i, its half's Q4_K block of
+// each row through its own LDS-DMA ring. The h = 1 wave (issue priority 1) hands its accumulators
+// to its partner through LDS (ready / ack flags, 2 parities); the h = 0 wave adds them one unit
+// later, in a fixed order, and stores a partial slab per slice; the last slice to store a tile sums
+// its slabs in slice order (splitk_tiles_fixup, lk_kernels.hpp: deterministic, nobody waits).
 #pragma once
 
 #include "lk_kernels.hpp"
@@ -491,9 +490,11 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   }
   if (h == 0 && nunits > 0) collect(nunits - 1, prev);
   wait_vmcnt<0>();
-  if (g.rsync)  // the last slice to store a tile sums it (the fragment area is free since the prologue)
-    splitk_tiles_fixup<G::NW>(g.rsync, prs, g.slices, h == 0 ? p : -1, 4, t0, 4, nunits, (g.tiles_per_range + 3) / 4,
-                              (LK_LDS int *)xlds, g.M, g.N, N16, g.dst, g.d_nb0, g.d_nb1, lane);
+  if (g.rsync) {  // the last slice to store a tile sums it; stream p lists in parity 0 of its pair's hand-off
+    auto lst_of = [&](int s) __attribute__((always_inline)) { return (LK_LDS int *)(xch + s * NT * 64); };
+    splitk_tiles_fixup<G::NW>(g.rsync, prs, g.slices, h == 0 ? p : -1, 4, t0, 4, nunits, lst_of, g.M, g.N, N16, g.dst,
+                              g.d_nb0, g.d_nb1, lane);
+  }
 }
 
 

@@ -51,7 +51,7 @@ def test_is_gfx950_code_object(lib):
 # (DESIGN.md §3); lab variants are built from patched copies of csrc/, never into this library.
 PRODUCT_KERNELS = {
     "gemv_stream_kernel", "gemv_q_n1_kernel", "gemm_skinny_kernel", "gemm_skinny_pair_kernel",
-    "gemm_sk_kernel", "xsplit_kernel", "gemm_wide_kernel", "splitk_reduce_kernel", "f32_mfma_kernel", "f32_lds_kernel",
+    "gemm_sk_kernel", "gemm_kpart_kernel", "xsplit_kernel", "gemm_wide_kernel", "splitk_reduce_kernel", "f32_mfma_kernel", "f32_lds_kernel",
     "gemm_q_lds_kernel", "gemm_q_mfma_kernel", "kquant_n1_kernel", "kquant_nc_kernel",
     "kquant_gemv_kernel", "kquant_mul_mat_kernel", "mul_mat_generic_kernel", "dequantize_coop_kernel",
     "quantize_coop_kernel", "dequantize_kernel", "quantize_kernel", "dot_direct_kernel",

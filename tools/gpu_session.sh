@@ -16,4 +16,8 @@ if [ -n "$AB_LIBS" ]; then
   ROUNDS=${ROUNDS:-2} bash tools/ab.sh "$AB_LIBS" $AB_SECTIONS
   rc=$?; echo "ab rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
+if [ -n "$AB_ENV" ]; then
+  ROUNDS=${ROUNDS:-2} bash tools/ab_env.sh "$AB_ENV" $AB_SECTIONS
+  rc=$?; echo "ab_env rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
 exit 0
