@@ -259,6 +259,39 @@ void lk_sharded_plan_destroy(lk_sharded_plan *plan);
 /* lk_sharded_plan_launch always issues its RCCL group, at one rank too (in-place copies), so the
  * one-GPU tests run the code a multi-GPU node runs. */
 
+/* ---- multi-GPU: the one-shot peer-write alternative ----------------
+ * Same partition as lk_sharded_plan, without a collective: rank r's push kernel writes its rows of
+ * every dst straight into every peer's full dst (xGMI stores, peer access enabled by the group)
+ * and adds 1 to the plan's arrival signal on every rank; the next plan launched in the group is
+ * gated on each rank by hipStreamWaitValue64(signal >= launches · P) — the command processor holds
+ * the queue, no kernel spins. One process drives the P ranks (the Kotlin host's shape).
+ *   lk_p2p_group_create: ranks 0..P-1 on devices[r] (P <= 8); devices may repeat (several ranks on
+ *     one GPU, each with its own buffers: the one-GPU tests); distinct devices must be peers.
+ *   lk_p2p_plan_create: a, b, dst hold P·n tensors, rank-major: a[r·n+i] rank r's rows of node i
+ *     (ne[1] = M_i / P), b[r·n+i] rank r's full activations, dst[r·n+i] rank r's full dst (dense
+ *     rows, M_i % P == 0), all on rank r's device.
+ *   lk_p2p_plan_launch: streams[r] on rank r's device; ranks on one device share one stream. Each
+ *     launch waits (per rank) for every rank's rows of the plan launched before it in the group —
+ *     plans launched in sequence form a chain of dependent stages, like a model's layers. Eager
+ *     only: LK_ERR_NOT_IMPLEMENTED while the stream is capturing (the gate values grow with every
+ *     launch; lk_sharded_plan is the graph-replayable path). A launch that fails part-way leaves
+ *     the group refusing further launches (LK_ERR_DEVICE).
+ *   lk_p2p_plan_signal: synchronizes rank's device, reads its arrival signal (launches · P when
+ *     every push arrived). Destroy plans only after the streams are synchronized.
+ * Same bytes in every rank's dst as lk_plan over the unsharded nodes. No reference counterpart
+ * beyond the archived row split's peer copies (archive/cuda/src/ggml-cuda.cu:521, :645-680). */
+typedef struct lk_p2p_group lk_p2p_group;
+typedef struct lk_p2p_plan lk_p2p_plan;
+int lk_p2p_group_create(int nranks, const int *devices, lk_p2p_group **out);
+int lk_p2p_group_nranks(const lk_p2p_group *g);
+void lk_p2p_group_destroy(lk_p2p_group *g);
+int lk_p2p_plan_create(lk_p2p_group *g, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
+                       lk_p2p_plan **out);
+int lk_p2p_plan_launch(lk_p2p_plan *plan, void *const *streams);
+uint64_t lk_p2p_plan_num_launches(const lk_p2p_plan *plan);
+int lk_p2p_plan_signal(lk_p2p_plan *plan, int rank, uint64_t *value);
+void lk_p2p_plan_destroy(lk_p2p_plan *plan);
+
 /* ---- graph residency over host buffers ---------------------------------------
  * GGMLComputeOps.computeGraph / computeMulMat (core/GGMLComputeOps.kt:2515-2652) for a
  * graph of n MUL_MAT nodes on host ByteArrays, kept device-resident between nodes

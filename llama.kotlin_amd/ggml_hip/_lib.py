@@ -85,6 +85,8 @@ EXPORTED_SYMBOLS = (
     "lk_comm_device", "lk_comm_num_collectives",
     "lk_comm_destroy", "lk_comm_abort", "lk_comm_group_start", "lk_comm_group_end",
     "lk_sharded_plan_create", "lk_sharded_plan_launch", "lk_sharded_plan_num_gathers", "lk_sharded_plan_destroy",
+    "lk_p2p_group_create", "lk_p2p_group_nranks", "lk_p2p_group_destroy", "lk_p2p_plan_create", "lk_p2p_plan_launch",
+    "lk_p2p_plan_num_launches", "lk_p2p_plan_signal", "lk_p2p_plan_destroy",
     "lk_dequantize_device", "lk_quantize_device", "lk_dot_direct", "lk_dot_direct_device",
     # include/lk_gguf.h
     "lk_gguf_open_memory", "lk_gguf_open_file", "lk_gguf_close", "lk_gguf_version", "lk_gguf_alignment",
@@ -168,6 +170,18 @@ def load():
     L.lk_sharded_plan_num_gathers.argtypes = [vp]
     L.lk_sharded_plan_destroy.argtypes = [vp]
     L.lk_sharded_plan_destroy.restype = None
+    if hasattr(L, "lk_p2p_plan_create"):  # (absent from round-3 lab builds loaded for A/B)
+        L.lk_p2p_group_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp)]
+        L.lk_p2p_group_nranks.argtypes = [vp]
+        L.lk_p2p_group_destroy.argtypes = [vp]
+        L.lk_p2p_group_destroy.restype = None
+        L.lk_p2p_plan_create.argtypes = [vp, P, P, P, ctypes.c_int, ctypes.POINTER(vp)]
+        L.lk_p2p_plan_launch.argtypes = [vp, ctypes.POINTER(vp)]
+        L.lk_p2p_plan_num_launches.argtypes = [vp]
+        L.lk_p2p_plan_num_launches.restype = ctypes.c_uint64
+        L.lk_p2p_plan_signal.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        L.lk_p2p_plan_destroy.argtypes = [vp]
+        L.lk_p2p_plan_destroy.restype = None
     L.lk_dequantize_device.argtypes = [P, vp, vp]
     L.lk_quantize_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp]
     L.lk_dot_direct.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, vp]

@@ -240,3 +240,92 @@ class ShardedMulMatPlan:
             self.close()
         except Exception:
             pass
+
+
+class P2PGroup:
+    """lk_p2p_group (include/lk_hip.h): ranks 0..P-1 on ``devices`` driven by this process, peer
+    access enabled between distinct devices. Devices may repeat (several ranks on one GPU)."""
+
+    def __init__(self, devices):
+        import ctypes
+        from . import _lib
+        n = len(devices)
+        devs = (ctypes.c_int * n)(*devices)
+        self._handle = ctypes.c_void_p()
+        _lib.check(_lib.load().lk_p2p_group_create(n, devs, ctypes.byref(self._handle)))
+        self.devices = list(devices)
+        self.nranks = n
+
+    def close(self):
+        if self._handle:
+            from . import _lib
+            _lib.load().lk_p2p_group_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class P2PMulMatPlan:
+    """lk_p2p_plan: the one-shot peer-write alternative to ShardedMulMatPlan. ``ranks[r]`` =
+    [(a_shard, b, dst_full)] for rank r (on rank r's device; ``ga`` one allocator or one per rank).
+    A launch computes every rank's rows in place, pushes them into every peer's dst and signals;
+    the next plan launched in the group waits (hipStreamWaitValue64) until they all arrived.
+    Eager only (HipDeviceError/NotImplemented while capturing)."""
+
+    def __init__(self, group: P2PGroup, ga, ranks):
+        import ctypes
+        from . import _lib
+        from .ops import to_lk
+        P = group.nranks
+        if len(ranks) != P or len({len(nodes) for nodes in ranks}) != 1:
+            raise ValueError("one node list of equal length per rank")
+        gas = ga if isinstance(ga, (list, tuple)) else [ga] * P
+        n = len(ranks[0])
+        A = (_lib.LkTensor * max(P * n, 1))()
+        B = (_lib.LkTensor * max(P * n, 1))()
+        D = (_lib.LkTensor * max(P * n, 1))()
+        for r, nodes in enumerate(ranks):
+            for i, (a, b, d) in enumerate(nodes):
+                A[r * n + i], B[r * n + i], D[r * n + i] = to_lk(gas[r], a), to_lk(gas[r], b), to_lk(gas[r], d)
+        self._handle = ctypes.c_void_p()
+        _lib.check(_lib.load().lk_p2p_plan_create(group._handle, A, B, D, n, ctypes.byref(self._handle)))
+        self.group = group
+
+    def launch(self, streams):
+        """``streams``: one torch stream per rank, or one stream for all (ranks on one device)."""
+        import ctypes
+        from . import _lib
+        P = self.group.nranks
+        if not isinstance(streams, (list, tuple)):
+            streams = [streams] * P
+        hs = (ctypes.c_void_p * P)(*[int(s.cuda_stream) for s in streams])
+        _lib.check(_lib.load().lk_p2p_plan_launch(self._handle, hs))
+
+    @property
+    def numLaunches(self) -> int:
+        from . import _lib
+        return int(_lib.load().lk_p2p_plan_num_launches(self._handle))
+
+    def signal(self, rank: int) -> int:
+        """Rank's arrival signal after synchronizing its device (launches · P when all arrived)."""
+        import ctypes
+        from . import _lib
+        v = ctypes.c_uint64()
+        _lib.check(_lib.load().lk_p2p_plan_signal(self._handle, rank, ctypes.byref(v)))
+        return int(v.value)
+
+    def close(self):
+        if self._handle:
+            from . import _lib
+            _lib.load().lk_p2p_plan_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
