@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--no-batched", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-multi-gpu-cost", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=6144)
     ap.add_argument("--sharded", action="store_true",
                     help="the N > 1 path (C-ABI RCCL communicator + lk_sharded_plan) at any world size")
@@ -287,6 +288,8 @@ def main():
         section("n1_configs", lambda: n1_configs(torch, G, dev))
         section("batched", lambda: batched(torch, G, dev))
         section("next_rows", lambda: next_rows(torch, G, dev))
+    if rank == 0 and world == 1 and not args.no_multi_gpu_cost:
+        section("multi_gpu_world1", lambda: multi_gpu_world1(torch, G, ga, nodes_by_layer, compute))
     if rank == 0 and world == 1 and not args.no_host_path:
         section("host_path_pcie", lambda: host_path(torch, G, dev))
     if waits:
@@ -432,6 +435,52 @@ def persistent_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, per_laye
     return {"tokens_per_s": round(1 / per, 2), "ms_per_token": round(per * 1e3, 4),
             "achieved_GBps": round(token_bytes / per / 1e9, 1), "stages_per_token": len(groups) * len(nodes_by_layer),
             "launches_per_token": 1, "hip_graph": g is not None, "tokens_timed": reps, "barrier_timeout": timed_out}
+
+
+def multi_gpu_world1(torch, G, ga, nodes_by_layer, stream, reps=5):
+    """The per-layer cost of the two multi-GPU exchange designs at world size 1, eager
+    (the one-shot path cannot be captured): the token's 32 layer launches enqueued behind a sleep
+    kernel (so the host's enqueue rate does not show), timed between events after it, as
+      plain      lk_plan per layer (no exchange);
+      rccl       lk_sharded_plan per layer: the launch + one RCCL group of 7 in-place all-gathers;
+      one_shot   lk_p2p_plan per layer: hipStreamWaitValue64 gate on the previous layer's signal,
+                 the launch, the push kernel (no copies at world 1, only the signal).
+    The differences to plain are each design's fixed per-layer cost on one GPU; xGMI transfer time
+    comes on top at P > 1 (DESIGN §6b's budget)."""
+    names = [n for (n, _, _) in LAYER_MATS]
+    plain = [G.MulMatPlan(ga, [n[k] for k in names]) for n in nodes_by_layer]
+    comm = G.Comm.single()
+    rccl = [G.ShardedMulMatPlan(comm, ga, [(G.shard_view(n[k][0], 1, 0), n[k][1], n[k][2]) for k in names])
+            for n in nodes_by_layer]
+    group = G.P2PGroup([torch.cuda.current_device()])
+    p2p = [G.P2PMulMatPlan(group, ga, [[(G.shard_view(n[k][0], 1, 0), n[k][1], n[k][2]) for k in names]])
+           for n in nodes_by_layer]
+    out = {}
+    for key, plans, launch in (("plain", plain, lambda p: p.launch(stream=stream)),
+                               ("rccl", rccl, lambda p: p.launch(stream=stream)),
+                               ("one_shot", p2p, lambda p: p.launch(stream))):
+        for p in plans:  # warm
+            launch(p)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(stream):
+                torch.cuda._sleep(20_000_000)  # ~10 ms: the host enqueues the token meanwhile
+                e0.record(stream)
+                for p in plans:
+                    launch(p)
+                e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3 / len(plans))
+        out[key + "_us_per_layer"] = round(sorted(ts)[len(ts) // 2], 3)
+    out["rccl_cost_us_per_layer"] = round(out["rccl_us_per_layer"] - out["plain_us_per_layer"], 3)
+    out["one_shot_cost_us_per_layer"] = round(out["one_shot_us_per_layer"] - out["plain_us_per_layer"], 3)
+    out["one_shot_signals_ok"] = all(p.signal(0) == p.numLaunches for p in p2p)
+    for p in p2p + rccl:
+        p.close()
+    group.close(); comm.close()
+    return out
 
 
 def headline(torch, G, dev, copies=48, reps=20):

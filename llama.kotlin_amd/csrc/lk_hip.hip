@@ -417,9 +417,12 @@ int splitk_counters(int slices, size_t slab_bytes, int64_t ntiles, bool list_ok,
 }
 
 // Activation fragments for the batched kernels (xsplit_kernel: a wave per kXsItems (x-tile, block) items).
-void launch_xsplit(const XSplitArgs &xa, hipStream_t st) {
+void launch_xsplit(const XSplitArgs &xa_in, hipStream_t st) {
+  XSplitArgs xa = xa_in;
   const int64_t ntx = (xa.N + 15) / 16, nblk = xa.K / 32, waves = (ntx * nblk + kXsItems - 1) / kXsItems;
-  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, xa);
+  xa.xblocks = (int32_t)((waves + 3) / 4);
+  const int64_t zblocks = xa.zero ? ((int64_t)xa.zM * ((xa.zN + 3) / 4) + 255) / 256 : 0;
+  hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)(xa.xblocks + zblocks)), dim3(256), 0, st, xa);
 }
 
 int grow(void **p, size_t *have, size_t want) {
@@ -717,7 +720,14 @@ int launch_kpart_t(const SkinnyArgs &s, hipStream_t st) {
   ranges = (ntile + tpr - 1) / tpr;
   g.tiles_per_range = tpr;
   g.slices = slices;
-  if (slices > 1) {
+  // two K slices (C3's N = 32 at K = 4096): each adds its tile sums into dst, zeroed by the xsplit
+  // launch — a + b is b + a, so the result does not depend on which slice adds first, and equals the
+  // slab sum s0 + s1 (only −0.0 + −0.0 becomes +0.0). More slices: slabs and the last arriver.
+  static const bool no_atomic = getenv_flag("LK_KPART_NO_ATOMIC");
+  g.atomic_dst = slices == 2 && !no_atomic;
+  if (g.atomic_dst) {
+    xa.zero = s.dst; xa.z_nb0 = s.d_nb0; xa.z_nb1 = s.d_nb1; xa.zM = s.M; xa.zN = s.N;
+  } else if (slices > 1) {
     const size_t slab_bytes = (size_t)slices * g.M * 16 * NT * sizeof(float);
     if (int rc = grow(&S.partial, &S.partial_bytes, slab_bytes)) return rc;
     g.partial = (float *)S.partial;
@@ -727,7 +737,7 @@ int launch_kpart_t(const SkinnyArgs &s, hipStream_t st) {
   launch_xsplit(xa, st);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_kpart_kernel<QT, NT>), dim3(grid), dim3(KG::NW * 64), KG::LDS, st, g);
-  if (slices > 1 && !g.tcnt) {
+  if (slices > 1 && !g.tcnt && !g.atomic_dst) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
                        slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);

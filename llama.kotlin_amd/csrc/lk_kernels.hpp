@@ -805,6 +805,11 @@ struct XSplitArgs {
   float *xsum;        // [nblk][N16]: mult · Σ_block x
   float mult;
   int32_t q4_order;   // 1: k order (0,2,4,6,1,3,5,7) within each 8; 2: (0,4,1,5,2,6,3,7) (lk_skinny.hpp)
+  // optional: blocks [xblocks, grid) zero dst(n, m) at n·z_nb0 + m·z_nb1, m < zM, n < zN (the GEMM that
+  // follows adds its two K slices into it: gemm_kpart_kernel's atomic_dst)
+  int32_t xblocks, zM, zN;
+  uint8_t *zero;
+  int64_t z_nb0, z_nb1;
 };
 
 // One wave per kXsItems consecutive (x-tile, block) items, every item's loads issued before any is
@@ -812,6 +817,20 @@ struct XSplitArgs {
 // in flight beat 4 waves with 32 loads each).
 constexpr int kXsItems = 1;
 __global__ __launch_bounds__(256) void xsplit_kernel(XSplitArgs g) {
+  if (g.zero && (int)blockIdx.x >= g.xblocks) {  // dst zeroing: 4 columns of one row per thread
+    const int c4 = (g.zN + 3) / 4;
+    const int64_t i = (int64_t)(blockIdx.x - g.xblocks) * 256 + threadIdx.x;
+    if (i >= (int64_t)g.zM * c4) return;
+    const int64_t m = i / c4;
+    const int n0 = (int)(i % c4) * 4;
+    uint8_t *o = g.zero + m * g.z_nb1 + n0 * g.z_nb0;
+    if (g.z_nb0 == 4 && n0 + 4 <= g.zN && (((uintptr_t)o) & 15) == 0) {
+      *(f32x4 *)o = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      for (int e = 0; e < 4 && n0 + e < g.zN; e++) *(float *)(o + e * g.z_nb0) = 0.f;
+    }
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int64_t nblk = g.K / 32, ntx = (g.N + 15) / 16, total = ntx * nblk;
   const int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kXsItems;

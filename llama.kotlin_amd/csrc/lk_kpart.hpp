@@ -69,6 +69,7 @@ struct KpartArgs {
   int32_t M, N, K;
   int32_t slices, tiles_per_range, tasks;  // tasks = ranges·slices (the grid is padded to 8)
   unsigned *tcnt;          // per-tile arrival counters (slices > 1), zero between launches
+  int32_t atomic_dst;      // slices == 2: tile sums added into dst (zeroed by the xsplit launch)
 };
 
 // LDS atomic add returning the old value (inline asm: the compiler would drain every LDS-DMA in
@@ -148,7 +149,11 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
   [[maybe_unused]] uint64_t c_wait = 0, c_comp = 0, c_red = 0;
   const int slice = task % g.slices, range = task / g.slices;
   const int nblk = g.K / 32;
-  const int kbw = slice * G::SPAN + wave * KB;                 // this wave's first block
+  // K part of this wave, rotated by the range: the 32 CUs of an XCD load their fragments in
+  // different orders (the same lines requested by every CU at once serialize on one L2 channel);
+  // partials are summed in part order, so the rotation changes no bit of the result
+  const int part = (wave + range) % NW;
+  const int kbw = slice * G::SPAN + part * KB;                 // this wave's first block
   const int nbw = max(0, min(KB, nblk - kbw));                 // its blocks (a short last slice)
   const int nact = min(NW, (min(G::SPAN, nblk - slice * G::SPAN) + KB - 1) / KB);  // waves with blocks
   const int64_t RB = (int64_t)nblk * BB;
@@ -284,7 +289,7 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
     // slot's previous tile, u − NB, was summed), counted in; the wave completing the count sums
     const int rs = u % NB;
     while (ldsk_ld(done + rs) < u - NB) __builtin_amdgcn_s_sleep(1);
-    LK_LDS f32x4 *mine = red + ((rs * NW + wave) * NT) * 64 + lane;
+    LK_LDS f32x4 *mine = red + ((rs * NW + part) * NT) * 64 + lane;
 #pragma unroll
     for (int j = 0; j < NT; j++) mine[j * 64] = acc[j];
     unsigned before = 0;
@@ -302,6 +307,31 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
           const f32x4 o = pr[(w * NT + j) * 64];
           sum[j].x += o.x; sum[j].y += o.y; sum[j].z += o.z; sum[j].w += o.w;
         }
+      if (g.atomic_dst) {
+        // two K slices: add the tile into dst. Through LDS first (the slot's own partial area, every
+        // part already read: LDS ops of a wave run in order) into rows of pitch N16 + 4 floats
+        // (conflict-free 16-B writes), read back so that each atomic wave-instruction adds 64 / N16
+        // whole dst rows — 256 contiguous bytes at N16 = 32, the full-rate shape. Lanes past M or N
+        // add +0.0 to a valid element (a no-op: the running sum starts at +0.0 and never becomes
+        // −0.0), so every lane issues exactly N16 / 4 atomics (counted in st_hist).
+        constexpr int PT = 16 * NT + 4;
+        LK_LDS float *trows = (LK_LDS float *)(red + (rs * NW * NT) * 64);
+#pragma unroll
+        for (int j = 0; j < NT; j++) *(LK_LDS f32x4 *)(trows + (lane & 15) * PT + 16 * j + 4 * (lane >> 4)) = sum[j];
+#pragma unroll
+        for (int i = 0; i < NT * 4; i++) {
+          const int idx = i * 64 + lane, ml = idx / (16 * NT), n = idx % (16 * NT);
+          const int64_t m = (int64_t)(t0 + u) * 16 + ml;
+          const bool ok = m < g.M && n < g.N;
+          const float v = ok ? trows[ml * PT + n] : 0.f;
+          const int64_t mc = ok ? m : 0, nc = ok ? n : 0;
+          __hip_atomic_fetch_add((float *)(g.dst + mc * g.d_nb1 + nc * g.d_nb0), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ldsk_st((LK_LDS int *)cnt + rs, 0);
+        ldsk_st(done + rs, u);
+        st_hist = (st_hist << 8) | (NT * 4);
+        continue;
+      }
       ldsk_st((LK_LDS int *)cnt + rs, 0);
       ldsk_st(done + rs, u);
       // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))

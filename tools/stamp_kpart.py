@@ -76,6 +76,24 @@ def main():
                     v = a[:, :, k][live] / 100.0 / np.maximum(units, 1)
                     out[ph] = round(float(np.median(v)), 3)
             out["units_med"] = float(np.median(units))
+            if not pair:  # per workgroup: who ends the loop late, and why (entry, start or compute)
+                wgs = np.nonzero(live.any(axis=1))[0]
+                grid = (len(wgs) + 7) // 8 * 8
+                rows = []
+                for b in wgs:
+                    lv = live[b]
+                    rows.append({"bid": int(b), "xcd": int(b % 8), "task": int((b % 8) * (grid // 8) + b // 8),
+                                 "entry": round(float((a[b, lv, 0].min() - t0) / 100), 2),
+                                 "loop_start": round(float((a[b, lv, 2].max() - t0) / 100), 2),
+                                 "loop_end": round(float((a[b, lv, 3].max() - t0) / 100), 2),
+                                 "comp_per_unit": round(float(np.median(a[b, lv, 6] / np.maximum(a[b, lv, 8], 1))) / 100, 3),
+                                 "wait_per_unit": round(float(np.median(a[b, lv, 5] / np.maximum(a[b, lv, 8], 1))) / 100, 3),
+                                 "red_per_unit": round(float(np.median(a[b, lv, 7] / np.maximum(a[b, lv, 8], 1))) / 100, 3)})
+                rows.sort(key=lambda r: -r["loop_end"])
+                out["slowest_wgs"] = rows[:10]
+                out["fastest_wgs"] = rows[-3:]
+                out["loop_end_by_xcd"] = {x: round(float(np.median([r["loop_end"] for r in rows if r["xcd"] == x])), 2)
+                                          for x in range(8)}
             res[f"{qn}_11008x4096_n{N}"] = out
             del g
     print(json.dumps(res), flush=True)
