@@ -34,6 +34,18 @@ namespace lk {
 // 3 loop end, 4 exit — and sums over the wave's units: 5 ring wait, 6 compute, 7 tile sum (slot wait,
 // partial, count, the completing wave's sum and stores), 8 units. Read by tools/stamp_kpart.py.
 
+#ifndef LK_KP_ACC_MIX
+#define LK_KP_ACC_MIX 0  // lab builds only: the per-block scale as four v_fma_mix_f32 (round-4 first version)
+#endif
+#ifndef LK_KP_PRIO
+#define LK_KP_PRIO 0  // lab builds only (tools/build_lab.sh): issue-priority policies of the SIMD's two waves
+#endif
+
+// The waits of gemm_kpart_kernel are on waves of the SAME workgroup (LDS words), which are always
+// co-resident: they end by construction. A fixed 200 ms bound (not lk_sync_wait_bound, the test
+// hook of the cross-workgroup waits) still turns a logic error into a counted timeout, not a hang.
+constexpr uint64_t kIntraWgBound = 20000000ull;
+
 template <int QT, int NT> struct KpartGeom {
   static constexpr int NW = 8;
   static constexpr int BB = QTraits<QT>::BB;
@@ -46,7 +58,7 @@ template <int QT, int NT> struct KpartGeom {
   static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : 3;
   static constexpr int NB = 4;                        // tile slots (tiles in flight in the workgroup)
   static constexpr int RED = NB * NW * NT * 64 * 16;  // partial tiles, [slot][wave][j][lane]
-  static constexpr int FL = 64;                       // cnt[NB], done[NB]
+  static constexpr int FL = 64;                       // cnt[NB], claim[NB], done[NB]
   static constexpr int DFIT = (kLdsBytes - RED - FL) / (NW * SLOT);
   static constexpr int D = DFIT > 3 ? 3 : DFIT;       // ring depth (units in flight per wave)
   static constexpr int LDS = RED + FL + NW * D * SLOT;
@@ -91,6 +103,16 @@ __device__ __forceinline__ void ldsk_st(LK_LDS int *p, int v) {
   asm volatile("" ::: "memory");
 }
 
+// acc += s·p as two packed FMAs (v_pk_fma_f32, the scale converted once per block) instead of four
+// mixed-precision FMAs
+__device__ __forceinline__ void accumulate_pk(f32x4 &acc, float s, f32x4 p) {
+  const f2v s2 = {s, s};
+  f2v lo = {acc.x, acc.y}, hi = {acc.z, acc.w};
+  lo = __builtin_elementwise_fma(s2, f2v{p.x, p.y}, lo);
+  hi = __builtin_elementwise_fma(s2, f2v{p.z, p.w}, hi);
+  acc = f32x4{lo.x, lo.y, hi.x, hi.y};
+}
+
 // Block B of a wave's KB: weight fragment from its dwords, the MFMA pair against the held fragments,
 // acc += s·p (the offset term comes once per unit, kpart_offsets).
 template <int QT, int NT, int KB, int B, int WPB>
@@ -115,7 +137,8 @@ __device__ __forceinline__ void kpart_block(const uint32_t (&w)[WPB], const u32x
   for (int j = 0; j < NT; j++) {
     f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
-    accumulate_s<false>(acc[j], s1, 0.f, p, p);
+    if constexpr (LK_KP_ACC_MIX || NT == 1) accumulate_s<false>(acc[j], s1, 0.f, p, p);  // NT = 1: packed spills
+    else accumulate_pk(acc[j], s1, p);
   }
 }
 
@@ -137,7 +160,8 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
   LK_LDS uint8_t *const sbase = (LK_LDS uint8_t *)(LK_LDS void *)smem;
   LK_LDS f32x4 *red = (LK_LDS f32x4 *)sbase;                         // [NB][NW][NT][64]
   LK_LDS unsigned *cnt = (LK_LDS unsigned *)(sbase + G::RED);        // per slot: partials counted in
-  LK_LDS int *done = (LK_LDS int *)(sbase + G::RED) + NB;            // per slot: last unit summed
+  LK_LDS unsigned *claim = cnt + NB;                                 // per slot: a summer's claim
+  LK_LDS int *done = (LK_LDS int *)(sbase + G::RED) + 2 * NB;        // per slot: last unit summed
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t *ring = smem + G::RED + G::FL + wave * D * G::SLOT;
@@ -161,8 +185,8 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
   const int t0 = range * g.tiles_per_range, t1 = min(t0 + g.tiles_per_range, ntile);
   const int nunits = nbw > 0 ? t1 - t0 : 0;                    // every tile of the range, in order
   const int pp = nbw * BB / 16;                                // cells of this wave's row piece
-  // counters 0; done = −1: the first use of slot rs (unit rs) has no predecessor to wait for
-  if (threadIdx.x < 2 * NB) ldsk_st((LK_LDS int *)cnt + threadIdx.x, threadIdx.x < NB ? 0 : -1);
+  // counts and claims 0; done[s] = s − NB: slot s first holds unit s, with no predecessor to wait for
+  if (threadIdx.x < 3 * NB) ldsk_st((LK_LDS int *)cnt + threadIdx.x, threadIdx.x < 2 * NB ? 0 : (int)threadIdx.x - 3 * NB);
 
   // unit u = rows of tile t0 + u, bytes [kbw·BB, + nbw·BB) of each; cell q = r·PP + c lands at
   // slot + 16q (row pitch PIECE); cells past the unit re-read cell 0
@@ -238,9 +262,110 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
   // stores this wave issued after each of its last D DMA issues (its tile sums), for the ring waits
   int st_hist = 0;  // 8 bits per unit, newest in the low byte
   uint64_t red_mask = 0;  // units whose tile this wave summed and stored (nunits <= 64, host-checked)
+  // Tile sums are claimed, not assigned (kpart_claims): any wave at a unit boundary, waiting for a
+  // slot, or done with its units sums a COMPLETE tile (all nact partials counted in) — in part order,
+  // so which wave sums it changes no bit — except the tile it has just completed itself: the wave
+  // completing a tile is the slowest one, and the sum would keep it the slowest. A claim is an LDS
+  // add on the slot's claim word (old value 0 wins), checked against the count afterwards (the slot
+  // may have been summed and refilled between the two); the summer re-arms count, done, claim in
+  // that order. Returns the store / atomic instructions issued (for the ring waits).
+  auto sum_tile = [&](int s, int ut) __attribute__((always_inline)) -> int {
+    f32x4 sum[NT];
+    const LK_LDS f32x4 *pr = red + (s * NW * NT) * 64 + lane;
+#pragma unroll
+    for (int w0 = 0; w0 < NW; w0 += 4) {  // four parts' reads in flight; an idle part's stale slot is not added
+      f32x4 v[4][NT];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int j = 0; j < NT; j++) v[q][j] = pr[((w0 + q) * NT + j) * 64];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+          if (w0 + q == 0) sum[j] = v[q][j];  // part 0 as is (−0.0 stays)
+          else if (w0 + q < nact) {
+            sum[j].x += v[q][j].x; sum[j].y += v[q][j].y; sum[j].z += v[q][j].z; sum[j].w += v[q][j].w;
+          }
+        }
+    }
+    int ns = NT;  // a lower bound of the store instructions issued (each j issues at least one)
+    if (g.atomic_dst) {
+      // two K slices: add the tile into dst. Through LDS first (the slot's own partial area, every
+      // part already read: LDS ops of a wave run in order) into rows of pitch N16 + 4 floats
+      // (conflict-free 16-B writes), read back so that each atomic wave-instruction adds 64 / N16
+      // whole dst rows — 256 contiguous bytes at N16 = 32, the full-rate shape. Lanes past M or N
+      // add +0.0 to a valid element (a no-op: the running sum starts at +0.0 and never becomes
+      // −0.0), so every lane issues exactly N16 / 4 atomics.
+      constexpr int PT = 16 * NT + 4, RPI = 64 / (16 * NT);
+      LK_LDS float *trows = (LK_LDS float *)(red + (s * NW * NT) * 64);
+#pragma unroll
+      for (int j = 0; j < NT; j++) *(LK_LDS f32x4 *)(trows + (lane & 15) * PT + 16 * j + 4 * (lane >> 4)) = sum[j];
+      const int ml0 = lane / (16 * NT), n = lane % (16 * NT);
+      float v[NT * 4];
+#pragma unroll
+      for (int i = 0; i < NT * 4; i++) v[i] = trows[(i * RPI + ml0) * PT + n];
+      const int64_t mt = (int64_t)(t0 + ut) * 16 + ml0;
+      uint8_t *const lane_dst = g.dst + mt * g.d_nb1 + (int64_t)n * g.d_nb0;
+#pragma unroll
+      for (int i = 0; i < NT * 4; i++) {
+        const bool ok = mt + i * RPI < g.M && n < g.N;
+        float *const o = ok ? (float *)(lane_dst + (int64_t)(i * RPI) * g.d_nb1) : (float *)g.dst;
+        __hip_atomic_fetch_add(o, ok ? v[i] : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ns = NT * 4;
+    } else {
+      // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
+      const int64_t m = (int64_t)(t0 + ut) * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NT; j++) {
+        const int n0 = 16 * j + 4 * (lane >> 4);
+        if (g.slices > 1) {
+          if (m < g.M) store_partial(g.tcnt != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, sum[j]);
+        } else if (m < g.M) {
+          const float e4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
+          if (g.d_nb0 == 4 && n0 + 4 <= g.N && (((uintptr_t)(g.dst + m * g.d_nb1 + n0 * 4)) & 15) == 0) {
+            *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = sum[j];
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+              if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
+          }
+        }
+      }
+      red_mask |= 1ull << ut;
+    }
+    ldsk_st((LK_LDS int *)cnt + s, 0);
+    ldsk_st(done + s, ut);
+    ldsk_st((LK_LDS int *)claim + s, 0);
+    return ns;
+  };
+  auto try_claims = [&](int skip) __attribute__((always_inline)) -> int {
+    int ns = 0;
+    for (int s = 0; s < NB; s++) {
+      if (ldsk_ld((const LK_LDS int *)cnt + s) != nact) continue;
+      unsigned old = 0;
+      if (lane == 0) old = lds_add_rtn(claim + s, 1u);
+      if (__builtin_amdgcn_readfirstlane(old) != 0u) continue;
+      const int ut = ldsk_ld(done + s) + NB;  // the slot's tile (count and done read after the claim)
+      if (ldsk_ld((const LK_LDS int *)cnt + s) != nact || ut == skip) {
+        ldsk_st((LK_LDS int *)claim + s, 0);
+        continue;
+      }
+      ns += sum_tile(s, ut);
+    }
+    return ns;
+  };
   [[maybe_unused]] const uint64_t t_loop = LK_KP_T();
+#if LK_KP_PRIO == 1
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // lab: the younger wave of each SIMD first
+#endif
   for (int u = 0; u < nunits; u++) {
     [[maybe_unused]] const uint64_t ta = LK_KP_T();
+#if LK_KP_PRIO == 2
+    if ((u + (wave >> 2)) & 1) __builtin_amdgcn_s_setprio(1);  // lab: the SIMD's two waves take turns
+    else __builtin_amdgcn_s_setprio(0);
+#endif
     const int slot = u % D;
     f32x4 acc[NT];
 #pragma unroll
@@ -285,80 +410,49 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
 #endif
     }
     [[maybe_unused]] const uint64_t tr = LK_KP_T();
-    // the workgroup's sum of tile t0 + u: this wave's partial into tile slot u % NB (free once the
-    // slot's previous tile, u − NB, was summed), counted in; the wave completing the count sums
+    // the workgroup's sum of tile t0 + u: this wave's partial into slot u % NB (free once the slot's
+    // previous tile, u − NB, is summed: help sum complete tiles meanwhile), counted in; then claim
+    // complete tiles other than the one this wave may just have completed (kpart_claims)
     const int rs = u % NB;
-    while (ldsk_ld(done + rs) < u - NB) __builtin_amdgcn_s_sleep(1);
+    int nst = 0;
+    for (uint64_t tw = 0; ldsk_ld(done + rs) < u - NB;) {  // waits on waves of this workgroup only
+      nst += try_claims(-1);
+      __builtin_amdgcn_s_sleep(1);
+      if (!tw) tw = __builtin_amdgcn_s_memrealtime();
+      else if (__builtin_amdgcn_s_memrealtime() - tw >= kIntraWgBound) {
+        if (lane == 0) lk_note_timeout();
+        break;
+      }
+    }
     LK_LDS f32x4 *mine = red + ((rs * NW + part) * NT) * 64 + lane;
 #pragma unroll
     for (int j = 0; j < NT; j++) mine[j * 64] = acc[j];
     unsigned before = 0;
     if (lane == 0) before = lds_add_rtn(cnt + rs, 1u);
     before = __builtin_amdgcn_readfirstlane(before);
-    int nst = 0;
-    if (before + 1u == (unsigned)nact) {
-      f32x4 sum[NT];
-      const LK_LDS f32x4 *pr = red + (rs * NW * NT) * 64 + lane;
-#pragma unroll
-      for (int j = 0; j < NT; j++) sum[j] = pr[j * 64];  // wave 0's partial as is (-0.0 stays)
-      for (int w = 1; w < nact; w++)
-#pragma unroll
-        for (int j = 0; j < NT; j++) {
-          const f32x4 o = pr[(w * NT + j) * 64];
-          sum[j].x += o.x; sum[j].y += o.y; sum[j].z += o.z; sum[j].w += o.w;
-        }
-      if (g.atomic_dst) {
-        // two K slices: add the tile into dst. Through LDS first (the slot's own partial area, every
-        // part already read: LDS ops of a wave run in order) into rows of pitch N16 + 4 floats
-        // (conflict-free 16-B writes), read back so that each atomic wave-instruction adds 64 / N16
-        // whole dst rows — 256 contiguous bytes at N16 = 32, the full-rate shape. Lanes past M or N
-        // add +0.0 to a valid element (a no-op: the running sum starts at +0.0 and never becomes
-        // −0.0), so every lane issues exactly N16 / 4 atomics (counted in st_hist).
-        constexpr int PT = 16 * NT + 4;
-        LK_LDS float *trows = (LK_LDS float *)(red + (rs * NW * NT) * 64);
-#pragma unroll
-        for (int j = 0; j < NT; j++) *(LK_LDS f32x4 *)(trows + (lane & 15) * PT + 16 * j + 4 * (lane >> 4)) = sum[j];
-#pragma unroll
-        for (int i = 0; i < NT * 4; i++) {
-          const int idx = i * 64 + lane, ml = idx / (16 * NT), n = idx % (16 * NT);
-          const int64_t m = (int64_t)(t0 + u) * 16 + ml;
-          const bool ok = m < g.M && n < g.N;
-          const float v = ok ? trows[ml * PT + n] : 0.f;
-          const int64_t mc = ok ? m : 0, nc = ok ? n : 0;
-          __hip_atomic_fetch_add((float *)(g.dst + mc * g.d_nb1 + nc * g.d_nb0), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        ldsk_st((LK_LDS int *)cnt + rs, 0);
-        ldsk_st(done + rs, u);
-        st_hist = (st_hist << 8) | (NT * 4);
-        continue;
-      }
-      ldsk_st((LK_LDS int *)cnt + rs, 0);
-      ldsk_st(done + rs, u);
-      // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
-      const int64_t m = (int64_t)(t0 + u) * 16 + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < NT; j++) {
-        const int n0 = 16 * j + 4 * (lane >> 4);
-        if (g.slices > 1) {
-          if (m < g.M) store_partial(g.tcnt != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, sum[j]);
-        } else if (m < g.M) {
-          const float e4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
-          if (g.d_nb0 == 4 && n0 + 4 <= g.N && (((uintptr_t)(g.dst + m * g.d_nb1 + n0 * 4)) & 15) == 0) {
-            *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = sum[j];
-          } else {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-              if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
-          }
-        }
-      }
-      nst = NT;  // a lower bound of the store instructions issued (each j issues at least one)
-      red_mask |= 1ull << u;
-    }
-    st_hist = (st_hist << 8) | nst;
+    nst += try_claims(before + 1u == (unsigned)nact ? u : -1);
+    st_hist = (st_hist << 8) | min(nst, 255);
 #ifdef LK_LAB_STAMPS
     c_red += LK_KP_T() - tr;
 #endif
+  }
+  // every tile of the range summed before the fix-up: claim what completes, the last tile included
+  if (nunits > 0) {
+    for (uint64_t tw = 0;;) {
+      (void)try_claims(-1);
+      bool all = true;
+      for (int k = 0; k < min(NB, nunits); k++) {
+        const int ut = nunits - 1 - k;
+        all = all && ldsk_ld(done + ut % NB) >= ut;
+      }
+      if (all) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (!tw) tw = __builtin_amdgcn_s_memrealtime();
+      else if (__builtin_amdgcn_s_memrealtime() - tw >= kIntraWgBound) {
+        if (lane == 0) lk_note_timeout();
+        break;
+      }
+    }
   }
   [[maybe_unused]] const uint64_t t_end = LK_KP_T();
   wait_vmcnt<0>();  // this wave's tile stores are done

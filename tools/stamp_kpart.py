@@ -91,6 +91,12 @@ def main():
                                  "red_per_unit": round(float(np.median(a[b, lv, 7] / np.maximum(a[b, lv, 8], 1))) / 100, 3)})
                 rows.sort(key=lambda r: -r["loop_end"])
                 out["slowest_wgs"] = rows[:10]
+                b = rows[0]["bid"]
+                out["slowest_wg_waves"] = [{"wave": w, "loop_start": round(float((a[b, w, 2] - t0) / 100), 2),
+                                            "loop_end": round(float((a[b, w, 3] - t0) / 100), 2),
+                                            "wait": round(float(a[b, w, 5] / 100), 2), "comp": round(float(a[b, w, 6] / 100), 2),
+                                            "red": round(float(a[b, w, 7] / 100), 2), "units": int(a[b, w, 8])}
+                                           for w in range(8) if live[b, w]]
                 out["fastest_wgs"] = rows[-3:]
                 out["loop_end_by_xcd"] = {x: round(float(np.median([r["loop_end"] for r in rows if r["xcd"] == x])), 2)
                                           for x in range(8)}
