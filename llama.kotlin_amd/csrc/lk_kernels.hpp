@@ -278,6 +278,18 @@ constexpr int kStreamMaxUnits = 3;   // units per row held in VGPRs: K <= 12288
 // A workgroup's piece of one node: rows [row_begin, row_end) of the node, with the node's
 // operands inlined so a workgroup reaches its first weight load after one scalar load.
 // Workgroup g owns slots work[g*spw .. g*spw + work[g*spw].count).
+// Lab timelines (built only with -DLK_LAB_STAMPS by tools/build_lab.sh, never in the product
+// library): per (workgroup, wave) s_memrealtime stamps and per-wave sums, read by lk_lab_stamps
+// (lk_hip.hip) into tools/stamp_kpart.py. Slot meanings are the kernel's (see its LK_KP_SET calls).
+#ifdef LK_LAB_STAMPS
+__device__ uint64_t lk_kp_stamps[1024][8][10];
+#define LK_KP_T() __builtin_amdgcn_s_memrealtime()
+#define LK_KP_SET(i, v) do { if (lane == 0 && blockIdx.x < 1024) lk_kp_stamps[blockIdx.x][wave][i] = (v); } while (0)
+#else
+#define LK_KP_T() 0ull
+#define LK_KP_SET(i, v) do { } while (0)
+#endif
+
 struct StreamWork {
   const uint8_t *a;
   const float *x;
@@ -449,6 +461,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
   extern __shared__ f32x4 lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  [[maybe_unused]] const uint64_t t_entry = LK_KP_T();
+  [[maybe_unused]] int st_units = 0;
   uint8_t *ring = (uint8_t *)lds + G::IMG + wave * (G::D * G::SLOT);
   float *q63 = (float *)((uint8_t *)lds + G::TOFF);  // K-quants only; published by the prologue's barrier
   if constexpr (QT == LK_TYPE_Q4_K)
@@ -491,6 +505,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     const int r0 = __builtin_amdgcn_readfirstlane(min(rb + wave * per_w, re));
     const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + per_w, re) - r0);
     const int nunits = nrows * nch;
+    st_units += nunits;
     const LK_GLOBAL uint8_t *A = (const LK_GLOBAL uint8_t *)a_node + (int64_t)r0 * RB;
 
     // 1. prologue, all by LDS-DMA:
@@ -746,6 +761,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       }
     }
   }
+  LK_KP_SET(0, t_entry); LK_KP_SET(4, LK_KP_T()); LK_KP_SET(8, (uint64_t)st_units);
   if (sync) {
     // chain plans: the workgroup that leaves last (every workgroup has passed every barrier)
     // re-arms the counters for the next launch (stream order makes the stores visible to it)
@@ -1477,17 +1493,6 @@ __device__ __forceinline__ void skinny_blocks(const uint32_t (&w)[SB][WPB], cons
   }
 }
 
-// Lab timelines (built only with -DLK_LAB_STAMPS by tools/build_lab.sh, never in the product
-// library): per (workgroup, wave) s_memrealtime stamps and per-wave sums, read by lk_lab_stamps
-// (lk_hip.hip) into tools/stamp_kpart.py. Slot meanings are the kernel's (see its LK_KP_SET calls).
-#ifdef LK_LAB_STAMPS
-__device__ uint64_t lk_kp_stamps[1024][8][10];
-#define LK_KP_T() __builtin_amdgcn_s_memrealtime()
-#define LK_KP_SET(i, v) do { if (lane == 0 && blockIdx.x < 1024) lk_kp_stamps[blockIdx.x][wave][i] = (v); } while (0)
-#else
-#define LK_KP_T() 0ull
-#define LK_KP_SET(i, v) do { } while (0)
-#endif
 
 // Split-K fix-up by the last arriver (round 4; the skinny kernels, gemm_sk_kernel, gemm_wide_kernel).
 // Nobody waits for anybody: grids larger than the CUs that are free, and launches sharing the GPU

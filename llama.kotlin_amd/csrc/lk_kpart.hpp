@@ -34,9 +34,6 @@ namespace lk {
 // 3 loop end, 4 exit — and sums over the wave's units: 5 ring wait, 6 compute, 7 tile sum (slot wait,
 // partial, count, the completing wave's sum and stores), 8 units. Read by tools/stamp_kpart.py.
 
-#ifndef LK_KP_ACC_MIX
-#define LK_KP_ACC_MIX 0  // lab builds only: the per-block scale as four v_fma_mix_f32 (round-4 first version)
-#endif
 #ifndef LK_KP_PRIO
 #define LK_KP_PRIO 0  // lab builds only (tools/build_lab.sh): issue-priority policies of the SIMD's two waves
 #endif
@@ -57,13 +54,14 @@ template <int QT, int NT> struct KpartGeom {
   static constexpr int SLOT = L * 1024;
   static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : 3;
   static constexpr int NB = 4;                        // tile slots (tiles in flight in the workgroup)
-  static constexpr int RED = NB * NW * NT * 64 * 16;  // partial tiles, [slot][wave][j][lane]
-  static constexpr int FL = 64;                       // cnt[NB], claim[NB], done[NB]
+  static constexpr int PT = 16 * NT + 4;              // partial tile row pitch (floats): conflict-free 16-B writes
+  static constexpr int PART = 16 * PT * 4;            // bytes of one part's partial tile
+  static constexpr int RED = NB * NW * PART;          // partial tiles, [slot][part][row][PT]
+  static constexpr int FL = 64;                       // cnt[NB], done[NB]
   static constexpr int DFIT = (kLdsBytes - RED - FL) / (NW * SLOT);
   static constexpr int D = DFIT > 3 ? 3 : DFIT;       // ring depth (units in flight per wave)
   static constexpr int LDS = RED + FL + NW * D * SLOT;
   static constexpr int MAXW = L * (D - 1) + D * NT;   // largest vmcnt a wait needs
-  static constexpr int LIST = RED / 4 - 16;           // end-of-launch tile list capacity (ints)
   static_assert(PIECE % 16 == 0, "row pieces are whole DMA cells");
   static_assert(D >= 2, "ring must double-buffer");
   static_assert(LDS <= kLdsBytes, "LDS");
@@ -103,16 +101,6 @@ __device__ __forceinline__ void ldsk_st(LK_LDS int *p, int v) {
   asm volatile("" ::: "memory");
 }
 
-// acc += s·p as two packed FMAs (v_pk_fma_f32, the scale converted once per block) instead of four
-// mixed-precision FMAs
-__device__ __forceinline__ void accumulate_pk(f32x4 &acc, float s, f32x4 p) {
-  const f2v s2 = {s, s};
-  f2v lo = {acc.x, acc.y}, hi = {acc.z, acc.w};
-  lo = __builtin_elementwise_fma(s2, f2v{p.x, p.y}, lo);
-  hi = __builtin_elementwise_fma(s2, f2v{p.z, p.w}, hi);
-  acc = f32x4{lo.x, lo.y, hi.x, hi.y};
-}
-
 // Block B of a wave's KB: weight fragment from its dwords, the MFMA pair against the held fragments,
 // acc += s·p (the offset term comes once per unit, kpart_offsets).
 template <int QT, int NT, int KB, int B, int WPB>
@@ -137,8 +125,7 @@ __device__ __forceinline__ void kpart_block(const uint32_t (&w)[WPB], const u32x
   for (int j = 0; j < NT; j++) {
     f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
-    if constexpr (LK_KP_ACC_MIX || NT == 1) accumulate_s<false>(acc[j], s1, 0.f, p, p);  // NT = 1: packed spills
-    else accumulate_pk(acc[j], s1, p);
+    accumulate_s<false>(acc[j], s1, 0.f, p, p);
   }
 }
 
@@ -158,10 +145,9 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
   constexpr int BB = G::BB, KB = G::KB, D = G::D, L = G::L, NW = G::NW, NB = G::NB;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   LK_LDS uint8_t *const sbase = (LK_LDS uint8_t *)(LK_LDS void *)smem;
-  LK_LDS f32x4 *red = (LK_LDS f32x4 *)sbase;                         // [NB][NW][NT][64]
+  LK_LDS float *red = (LK_LDS float *)sbase;                         // [NB][NW][16][PT]
   LK_LDS unsigned *cnt = (LK_LDS unsigned *)(sbase + G::RED);        // per slot: partials counted in
-  LK_LDS unsigned *claim = cnt + NB;                                 // per slot: a summer's claim
-  LK_LDS int *done = (LK_LDS int *)(sbase + G::RED) + 2 * NB;        // per slot: last unit summed
+  LK_LDS int *done = (LK_LDS int *)(sbase + G::RED) + NB;            // per slot: last unit summed
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t *ring = smem + G::RED + G::FL + wave * D * G::SLOT;
@@ -185,8 +171,8 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
   const int t0 = range * g.tiles_per_range, t1 = min(t0 + g.tiles_per_range, ntile);
   const int nunits = nbw > 0 ? t1 - t0 : 0;                    // every tile of the range, in order
   const int pp = nbw * BB / 16;                                // cells of this wave's row piece
-  // counts and claims 0; done[s] = s − NB: slot s first holds unit s, with no predecessor to wait for
-  if (threadIdx.x < 3 * NB) ldsk_st((LK_LDS int *)cnt + threadIdx.x, threadIdx.x < 2 * NB ? 0 : (int)threadIdx.x - 3 * NB);
+  // counts 0; done[s] = s − NB: slot s first holds unit s, with no predecessor to wait for
+  if (threadIdx.x < 2 * NB) ldsk_st((LK_LDS int *)cnt + threadIdx.x, threadIdx.x < NB ? 0 : (int)threadIdx.x - 2 * NB);
 
   // unit u = rows of tile t0 + u, bytes [kbw·BB, + nbw·BB) of each; cell q = r·PP + c lands at
   // slot + 16q (row pitch PIECE); cells past the unit re-read cell 0
@@ -262,50 +248,38 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
   // stores this wave issued after each of its last D DMA issues (its tile sums), for the ring waits
   int st_hist = 0;  // 8 bits per unit, newest in the low byte
   uint64_t red_mask = 0;  // units whose tile this wave summed and stored (nunits <= 64, host-checked)
-  // Tile sums are claimed, not assigned (kpart_claims): any wave at a unit boundary, waiting for a
-  // slot, or done with its units sums a COMPLETE tile (all nact partials counted in) — in part order,
-  // so which wave sums it changes no bit — except the tile it has just completed itself: the wave
-  // completing a tile is the slowest one, and the sum would keep it the slowest. A claim is an LDS
-  // add on the slot's claim word (old value 0 wins), checked against the count afterwards (the slot
-  // may have been summed and refilled between the two); the summer re-arms count, done, claim in
-  // that order. Returns the store / atomic instructions issued (for the ring waits).
+  // The sum of a complete tile (all nact partials counted in), by the wave whose count completed it:
+  // every part's partial read at once (LDS round trips, not adds, are what a tile sum costs under
+  // the ring's DMA traffic), added in part order (so the K rotation changes no bit), then stored
+  // (slices == 1), written as this slice's slab, or added into dst (two slices). Returns the store
+  // / atomic instructions issued (for the ring waits).
   auto sum_tile = [&](int s, int ut) __attribute__((always_inline)) -> int {
-    f32x4 sum[NT];
-    const LK_LDS f32x4 *pr = red + (s * NW * NT) * 64 + lane;
+    // lane (row ml0 + i·RPI, column n) for i < NT·4: 64 / N16 whole rows per instruction
+    constexpr int RPI = 64 / (16 * NT);
+    const int ml0 = lane / (16 * NT), n = lane % (16 * NT);
+    const LK_LDS float *pr = red + (s * NW) * (16 * G::PT) + ml0 * G::PT + n;
+    float v[NT * 4];
+    {
+      float q[NW][NT * 4];  // every part at once (one LDS round trip); an idle part's stale slot is not added
 #pragma unroll
-    for (int w0 = 0; w0 < NW; w0 += 4) {  // four parts' reads in flight; an idle part's stale slot is not added
-      f32x4 v[4][NT];
+      for (int p = 0; p < NW; p++)
 #pragma unroll
-      for (int q = 0; q < 4; q++)
+        for (int i = 0; i < NT * 4; i++) q[p][i] = pr[p * 16 * G::PT + i * RPI * G::PT];
 #pragma unroll
-        for (int j = 0; j < NT; j++) v[q][j] = pr[((w0 + q) * NT + j) * 64];
+      for (int i = 0; i < NT * 4; i++) {
+        v[i] = q[0][i];  // part 0 as is (−0.0 stays)
 #pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int j = 0; j < NT; j++) {
-          if (w0 + q == 0) sum[j] = v[q][j];  // part 0 as is (−0.0 stays)
-          else if (w0 + q < nact) {
-            sum[j].x += v[q][j].x; sum[j].y += v[q][j].y; sum[j].z += v[q][j].z; sum[j].w += v[q][j].w;
-          }
-        }
+        for (int p = 1; p < NW; p++)
+          if (p < nact) v[i] += q[p][i];
+      }
     }
-    int ns = NT;  // a lower bound of the store instructions issued (each j issues at least one)
+    const int64_t mt = (int64_t)(t0 + ut) * 16 + ml0;
+    int ns;
     if (g.atomic_dst) {
-      // two K slices: add the tile into dst. Through LDS first (the slot's own partial area, every
-      // part already read: LDS ops of a wave run in order) into rows of pitch N16 + 4 floats
-      // (conflict-free 16-B writes), read back so that each atomic wave-instruction adds 64 / N16
-      // whole dst rows — 256 contiguous bytes at N16 = 32, the full-rate shape. Lanes past M or N
-      // add +0.0 to a valid element (a no-op: the running sum starts at +0.0 and never becomes
-      // −0.0), so every lane issues exactly N16 / 4 atomics.
-      constexpr int PT = 16 * NT + 4, RPI = 64 / (16 * NT);
-      LK_LDS float *trows = (LK_LDS float *)(red + (s * NW * NT) * 64);
-#pragma unroll
-      for (int j = 0; j < NT; j++) *(LK_LDS f32x4 *)(trows + (lane & 15) * PT + 16 * j + 4 * (lane >> 4)) = sum[j];
-      const int ml0 = lane / (16 * NT), n = lane % (16 * NT);
-      float v[NT * 4];
-#pragma unroll
-      for (int i = 0; i < NT * 4; i++) v[i] = trows[(i * RPI + ml0) * PT + n];
-      const int64_t mt = (int64_t)(t0 + ut) * 16 + ml0;
+      // two K slices: add into dst (zeroed by the xsplit launch); each wave-instruction adds 64 / N16
+      // whole dst rows (256 contiguous bytes at N16 = 32: the full-rate shape). Lanes past M or N add
+      // +0.0 to a valid element (a no-op: the running sum starts at +0.0 and never becomes −0.0), so
+      // every lane issues exactly N16 / 4 atomics.
       uint8_t *const lane_dst = g.dst + mt * g.d_nb1 + (int64_t)n * g.d_nb0;
 #pragma unroll
       for (int i = 0; i < NT * 4; i++) {
@@ -314,46 +288,33 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
         __hip_atomic_fetch_add(o, ok ? v[i] : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       ns = NT * 4;
-    } else {
-      // outputs: lane holds C'(n = 16j + 4(lane>>4) + e, m = 16t + (lane&15))
-      const int64_t m = (int64_t)(t0 + ut) * 16 + (lane & 15);
+    } else if (g.slices > 1) {
+      // this slice's slab rows [slice][M][N16] (write-through when the fix-up sums them in the launch)
 #pragma unroll
-      for (int j = 0; j < NT; j++) {
-        const int n0 = 16 * j + 4 * (lane >> 4);
-        if (g.slices > 1) {
-          if (m < g.M) store_partial(g.tcnt != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, sum[j]);
-        } else if (m < g.M) {
-          const float e4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
-          if (g.d_nb0 == 4 && n0 + 4 <= g.N && (((uintptr_t)(g.dst + m * g.d_nb1 + n0 * 4)) & 15) == 0) {
-            *(f32x4 *)(g.dst + m * g.d_nb1 + n0 * 4) = sum[j];
-          } else {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-              if (n0 + q < g.N) *(float *)(g.dst + m * g.d_nb1 + (n0 + q) * g.d_nb0) = e4[q];
-          }
+      for (int i = 0; i < NT * 4; i++) {
+        const int64_t m = mt + i * RPI;
+        if (m < g.M) {
+          const int64_t idx = ((int64_t)slice * g.M + m) * N16 + n;
+          if (g.tcnt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[i]), prs, (int)(idx * 4), 0, 16);
+          else g.partial[idx] = v[i];
         }
       }
       red_mask |= 1ull << ut;
+    } else {
+#pragma unroll
+      for (int i = 0; i < NT * 4; i++) {
+        const int64_t m = mt + i * RPI;
+        if (m < g.M && n < g.N) *(float *)(g.dst + m * g.d_nb1 + (int64_t)n * g.d_nb0) = v[i];
+      }
+    }
+    if (!g.atomic_dst) {
+      // store instructions certainly issued: those with lane 0's row inside M (lane 0 holds the
+      // instruction's smallest row and column 0); a lower bound keeps the ring waits safe
+      const int64_t left = (int64_t)g.M - (int64_t)(t0 + ut) * 16;
+      ns = (int)min((int64_t)(NT * 4), (left + RPI - 1) / RPI);
     }
     ldsk_st((LK_LDS int *)cnt + s, 0);
     ldsk_st(done + s, ut);
-    ldsk_st((LK_LDS int *)claim + s, 0);
-    return ns;
-  };
-  auto try_claims = [&](int skip) __attribute__((always_inline)) -> int {
-    int ns = 0;
-    for (int s = 0; s < NB; s++) {
-      if (ldsk_ld((const LK_LDS int *)cnt + s) != nact) continue;
-      unsigned old = 0;
-      if (lane == 0) old = lds_add_rtn(claim + s, 1u);
-      if (__builtin_amdgcn_readfirstlane(old) != 0u) continue;
-      const int ut = ldsk_ld(done + s) + NB;  // the slot's tile (count and done read after the claim)
-      if (ldsk_ld((const LK_LDS int *)cnt + s) != nact || ut == skip) {
-        ldsk_st((LK_LDS int *)claim + s, 0);
-        continue;
-      }
-      ns += sum_tile(s, ut);
-    }
     return ns;
   };
   [[maybe_unused]] const uint64_t t_loop = LK_KP_T();
@@ -411,12 +372,9 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
     }
     [[maybe_unused]] const uint64_t tr = LK_KP_T();
     // the workgroup's sum of tile t0 + u: this wave's partial into slot u % NB (free once the slot's
-    // previous tile, u − NB, is summed: help sum complete tiles meanwhile), counted in; then claim
-    // complete tiles other than the one this wave may just have completed (kpart_claims)
+    // previous tile, u − NB, was summed), counted in; the wave completing the count sums
     const int rs = u % NB;
-    int nst = 0;
     for (uint64_t tw = 0; ldsk_ld(done + rs) < u - NB;) {  // waits on waves of this workgroup only
-      nst += try_claims(-1);
       __builtin_amdgcn_s_sleep(1);
       if (!tw) tw = __builtin_amdgcn_s_memrealtime();
       else if (__builtin_amdgcn_s_memrealtime() - tw >= kIntraWgBound) {
@@ -424,35 +382,18 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
         break;
       }
     }
-    LK_LDS f32x4 *mine = red + ((rs * NW + part) * NT) * 64 + lane;
+    // this wave's partial: lane holds C'(n = 16j + 4(lane>>4) + e, m = lane & 15), as row-major rows
+    LK_LDS float *mine = red + (rs * NW + part) * (16 * G::PT) + (lane & 15) * G::PT + 4 * (lane >> 4);
 #pragma unroll
-    for (int j = 0; j < NT; j++) mine[j * 64] = acc[j];
+    for (int j = 0; j < NT; j++) *(LK_LDS f32x4 *)(mine + 16 * j) = acc[j];
     unsigned before = 0;
     if (lane == 0) before = lds_add_rtn(cnt + rs, 1u);
     before = __builtin_amdgcn_readfirstlane(before);
-    nst += try_claims(before + 1u == (unsigned)nact ? u : -1);
-    st_hist = (st_hist << 8) | min(nst, 255);
+    const int nst = before + 1u == (unsigned)nact ? sum_tile(rs, u) : 0;
+    st_hist = (st_hist << 8) | nst;
 #ifdef LK_LAB_STAMPS
     c_red += LK_KP_T() - tr;
 #endif
-  }
-  // every tile of the range summed before the fix-up: claim what completes, the last tile included
-  if (nunits > 0) {
-    for (uint64_t tw = 0;;) {
-      (void)try_claims(-1);
-      bool all = true;
-      for (int k = 0; k < min(NB, nunits); k++) {
-        const int ut = nunits - 1 - k;
-        all = all && ldsk_ld(done + ut % NB) >= ut;
-      }
-      if (all) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (!tw) tw = __builtin_amdgcn_s_memrealtime();
-      else if (__builtin_amdgcn_s_memrealtime() - tw >= kIntraWgBound) {
-        if (lane == 0) lk_note_timeout();
-        break;
-      }
-    }
   }
   [[maybe_unused]] const uint64_t t_end = LK_KP_T();
   wait_vmcnt<0>();  // this wave's tile stores are done
