@@ -42,6 +42,7 @@ namespace lk {
 // co-resident: they end by construction. A fixed 200 ms bound (not lk_sync_wait_bound, the test
 // hook of the cross-workgroup waits) still turns a logic error into a counted timeout, not a hang.
 constexpr uint64_t kIntraWgBound = 20000000ull;
+constexpr int kSumLag = 2;  // a tile's owner sums it at its own boundary this many units later
 
 template <int QT, int NT> struct KpartGeom {
   static constexpr int NW = 8;
@@ -317,6 +318,20 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
     ldsk_st(done + s, ut);
     return ns;
   };
+  // tile u complete: the slot's previous tile (u − NB) summed and all nact partials of u counted in
+  // (the summer resets the count before it publishes done)
+  auto wait_complete = [&](int u) __attribute__((always_inline)) {
+    const int s = u % NB;
+    for (uint64_t tw = 0; !(ldsk_ld(done + s) == u - NB && ldsk_ld((const LK_LDS int *)cnt + s) == nact);) {
+      __builtin_amdgcn_s_sleep(1);
+      if (!tw) tw = __builtin_amdgcn_s_memrealtime();
+      else if (__builtin_amdgcn_s_memrealtime() - tw >= kIntraWgBound) {
+        if (lane == 0) lk_note_timeout();
+        break;
+      }
+    }
+  };
+  int own = part;  // the next tile this wave sums (tiles u with u % nact == part)
   [[maybe_unused]] const uint64_t t_loop = LK_KP_T();
 #if LK_KP_PRIO == 1
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // lab: the younger wave of each SIMD first
@@ -372,7 +387,10 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
     }
     [[maybe_unused]] const uint64_t tr = LK_KP_T();
     // the workgroup's sum of tile t0 + u: this wave's partial into slot u % NB (free once the slot's
-    // previous tile, u − NB, was summed), counted in; the wave completing the count sums
+    // previous tile, u − NB, was summed), counted in; tile u is summed by its owner, the wave of part
+    // u % nact, at the owner's boundary u + kSumLag (or after its loop) — every wave sums ~1/nact of
+    // the tiles, none sums on the critical path of the slowest (round 4: the wave that completed a
+    // tile summed it, and since that wave is the slowest, all sums landed on the critical path)
     const int rs = u % NB;
     for (uint64_t tw = 0; ldsk_ld(done + rs) < u - NB;) {  // waits on waves of this workgroup only
       __builtin_amdgcn_s_sleep(1);
@@ -386,14 +404,22 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
     LK_LDS float *mine = red + (rs * NW + part) * (16 * G::PT) + (lane & 15) * G::PT + 4 * (lane >> 4);
 #pragma unroll
     for (int j = 0; j < NT; j++) *(LK_LDS f32x4 *)(mine + 16 * j) = acc[j];
-    unsigned before = 0;
-    if (lane == 0) before = lds_add_rtn(cnt + rs, 1u);
-    before = __builtin_amdgcn_readfirstlane(before);
-    const int nst = before + 1u == (unsigned)nact ? sum_tile(rs, u) : 0;
-    st_hist = (st_hist << 8) | nst;
+    if (lane == 0) (void)lds_add_rtn(cnt + rs, 1u);
+    int nst = 0;
+    while (own <= u - kSumLag) {
+      wait_complete(own);
+      nst += sum_tile(own % NB, own);
+      own += nact;
+    }
+    st_hist = (st_hist << 8) | min(nst, 255);
 #ifdef LK_LAB_STAMPS
     c_red += LK_KP_T() - tr;
 #endif
+  }
+  // the owned tiles left (the last ones: completed by the slowest wave)
+  for (; own < nunits; own += nact) {
+    wait_complete(own);
+    (void)sum_tile(own % NB, own);
   }
   [[maybe_unused]] const uint64_t t_end = LK_KP_T();
   wait_vmcnt<0>();  // this wave's tile stores are done
