@@ -34,6 +34,9 @@ namespace lk {
 // 3 loop end, 4 exit — and sums over the wave's units: 5 ring wait, 6 compute, 7 tile sum (slot wait,
 // partial, count, the completing wave's sum and stores), 8 units. Read by tools/stamp_kpart.py.
 
+#ifndef LK_KP_KB
+#define LK_KP_KB 0  // lab builds only: 16 = the first round-4 version (16 / NT blocks per wave)
+#endif
 #ifndef LK_KP_PRIO
 #define LK_KP_PRIO 0  // lab builds only (tools/build_lab.sh): issue-priority policies of the SIMD's two waves
 #endif
@@ -47,7 +50,10 @@ constexpr int kSumLag = 2;  // a tile's owner sums it at its own boundary this m
 template <int QT, int NT> struct KpartGeom {
   static constexpr int NW = 8;
   static constexpr int BB = QTraits<QT>::BB;
-  static constexpr int KB = 16 / NT;                  // blocks per wave (activations in 128 VGPRs)
+  // blocks per wave: 8 (activations in 64·NT VGPRs). At N <= 16 a wave could hold 16 (one slice
+  // spanning K = 4096), but the workgroup then loads 256 KB of fragments before its first unit and
+  // each unit is twice as long; 8 halves both and makes K = 4096 two slices added into dst
+  static constexpr int KB = LK_KP_KB ? LK_KP_KB / NT : 8;
   static constexpr int SPAN = NW * KB;                // blocks per workgroup (one K slice)
   static constexpr int PIECE = KB * BB;               // bytes of a wave's row piece
   static constexpr int PP = PIECE / 16;               // its 16-B cells
@@ -278,17 +284,13 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
     int ns;
     if (g.atomic_dst) {
       // two K slices: add into dst (zeroed by the xsplit launch); each wave-instruction adds 64 / N16
-      // whole dst rows (256 contiguous bytes at N16 = 32: the full-rate shape). Lanes past M or N add
-      // +0.0 to a valid element (a no-op: the running sum starts at +0.0 and never becomes −0.0), so
-      // every lane issues exactly N16 / 4 atomics.
+      // whole dst rows (256 contiguous bytes at N16 = N = 32: the full-rate shape). Lanes past M or N
+      // issue nothing (a shared dummy address would serialize every workgroup's idle lanes on one word)
       uint8_t *const lane_dst = g.dst + mt * g.d_nb1 + (int64_t)n * g.d_nb0;
 #pragma unroll
-      for (int i = 0; i < NT * 4; i++) {
-        const bool ok = mt + i * RPI < g.M && n < g.N;
-        float *const o = ok ? (float *)(lane_dst + (int64_t)(i * RPI) * g.d_nb1) : (float *)g.dst;
-        __hip_atomic_fetch_add(o, ok ? v[i] : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      ns = NT * 4;
+      for (int i = 0; i < NT * 4; i++)
+        if (mt + i * RPI < g.M && n < g.N)
+          __hip_atomic_fetch_add((float *)(lane_dst + (int64_t)(i * RPI) * g.d_nb1), v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (g.slices > 1) {
       // this slice's slab rows [slice][M][N16] (write-through when the fix-up sums them in the launch)
 #pragma unroll
@@ -308,9 +310,9 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
         if (m < g.M && n < g.N) *(float *)(g.dst + m * g.d_nb1 + (int64_t)n * g.d_nb0) = v[i];
       }
     }
-    if (!g.atomic_dst) {
-      // store instructions certainly issued: those with lane 0's row inside M (lane 0 holds the
-      // instruction's smallest row and column 0); a lower bound keeps the ring waits safe
+    {
+      // store / atomic instructions certainly issued: those with lane 0's row inside M (lane 0 holds
+      // the instruction's smallest row and column 0); a lower bound keeps the ring waits safe
       const int64_t left = (int64_t)g.M - (int64_t)(t0 + ut) * 16;
       ns = (int)min((int64_t)(NT * 4), (left + RPI - 1) / RPI);
     }
