@@ -34,6 +34,9 @@ namespace lk {
 // 3 loop end, 4 exit — and sums over the wave's units: 5 ring wait, 6 compute, 7 tile sum (slot wait,
 // partial, count, the completing wave's sum and stores), 8 units. Read by tools/stamp_kpart.py.
 
+#ifndef LK_KP_ACC_MIX
+#define LK_KP_ACC_MIX 0  // lab builds only: the per-block scale as four v_fma_mix_f32
+#endif
 #ifndef LK_KP_KB
 #define LK_KP_KB 0  // lab builds only: 16 = the first round-4 version (16 / NT blocks per wave)
 #endif
@@ -108,6 +111,16 @@ __device__ __forceinline__ void ldsk_st(LK_LDS int *p, int v) {
   asm volatile("" ::: "memory");
 }
 
+// acc += s·p as two packed FMAs (v_pk_fma_f32, the scale converted once per block) instead of four
+// mixed-precision FMAs
+__device__ __forceinline__ void accumulate_pk(f32x4 &acc, float s, f32x4 p) {
+  const f2v s2 = {s, s};
+  f2v lo = {acc.x, acc.y}, hi = {acc.z, acc.w};
+  lo = __builtin_elementwise_fma(s2, f2v{p.x, p.y}, lo);
+  hi = __builtin_elementwise_fma(s2, f2v{p.z, p.w}, hi);
+  acc = f32x4{lo.x, lo.y, hi.x, hi.y};
+}
+
 // Block B of a wave's KB: weight fragment from its dwords, the MFMA pair against the held fragments,
 // acc += s·p (the offset term comes once per unit, kpart_offsets).
 template <int QT, int NT, int KB, int B, int WPB>
@@ -132,7 +145,8 @@ __device__ __forceinline__ void kpart_block(const uint32_t (&w)[WPB], const u32x
   for (int j = 0; j < NT; j++) {
     f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[B][j]), wf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[B][j]), wf, p, 0, 0, 0);
-    accumulate_s<false>(acc[j], s1, 0.f, p, p);
+    if constexpr (LK_KP_ACC_MIX) accumulate_s<false>(acc[j], s1, 0.f, p, p);
+    else accumulate_pk(acc[j], s1, p);
   }
 }
 
@@ -272,12 +286,21 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
       for (int p = 0; p < NW; p++)
 #pragma unroll
         for (int i = 0; i < NT * 4; i++) q[p][i] = pr[p * 16 * G::PT + i * RPI * G::PT];
+      if (nact == NW) {  // every part active (uniform): plain adds, no selects
 #pragma unroll
-      for (int i = 0; i < NT * 4; i++) {
-        v[i] = q[0][i];  // part 0 as is (−0.0 stays)
+        for (int i = 0; i < NT * 4; i++) {
+          v[i] = q[0][i];  // part 0 as is (−0.0 stays)
 #pragma unroll
-        for (int p = 1; p < NW; p++)
-          if (p < nact) v[i] += q[p][i];
+          for (int p = 1; p < NW; p++) v[i] += q[p][i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NT * 4; i++) {
+          v[i] = q[0][i];
+#pragma unroll
+          for (int p = 1; p < NW; p++)
+            if (p < nact) v[i] += q[p][i];
+        }
       }
     }
     const int64_t mt = (int64_t)(t0 + ut) * 16 + ml0;
