@@ -465,11 +465,6 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
   [[maybe_unused]] int st_units = 0;
   uint8_t *ring = (uint8_t *)lds + G::IMG + wave * (G::D * G::SLOT);
   float *q63 = (float *)((uint8_t *)lds + G::TOFF);  // K-quants only; published by the prologue's barrier
-  int full_off[G::L];  // a whole unit's DMA lane offsets (lanes past the unit re-read its first 16 B)
-#pragma unroll
-  for (int j = 0; j < G::L; j++) full_off[j] = (j * 1024 + lane * 16 < G::UB) ? j * 1024 + lane * 16 : 0;
-  // this lane's 36 / 40 / 68 / … bytes inside ring slot 0 (a slot is G::SLOT further), as an LDS address
-  const uint32_t lane_ring = (uint32_t)(uintptr_t)(LK_LDS uint8_t *)(ring + lane * G::PB);
   if constexpr (QT == LK_TYPE_Q4_K)
     if (tid < 64) q63[tid] = __fdiv_rn((float)tid, 63.0f);
   if constexpr (QT == LK_TYPE_Q2_K)
@@ -531,13 +526,6 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     };
     auto dma_unit = [&](const LK_GLOBAL uint8_t *base, int ubytes, int sl) {
       LK_LDS uint8_t *slot = (LK_LDS uint8_t *)(ring + sl * G::SLOT);
-      if (ubytes == G::UB) {  // a whole unit (uniform): the lane offsets are fixed, no compares
-#pragma unroll
-        for (int j = 0; j < G::L; j++)
-          __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + full_off[j]), (LK_LDS void *)(slot + j * 1024), 16,
-                                           0, 2);
-        return;
-      }
 #pragma unroll
       for (int j = 0; j < G::L; j++) {
         int off = j * 1024 + lane * 16;
@@ -734,7 +722,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
           else __builtin_amdgcn_s_setprio(0);
           if (u + G::D - 1 < nunits) wait_vmcnt<G::VMCNT>();  // a full ring: D − 1 units issued past unit u
           else wait_vmcnt<0>();
-          const LK_LDS uint32_t *rp = (const LK_LDS uint32_t *)(uintptr_t)(lane_ring + slot * G::SLOT);
+          const uint32_t *rp = (const uint32_t *)(ring + slot * G::SLOT + lane * G::PB);
           uint32_t w[G::PDW];
           u32x4 kh, kc0, kc1;  // Q4_K: block lane/4's header and sub-blocks 2(lane%4), +1
           uint32_t q2s = 0, q2d = 0, q2c[4];  // Q2_K: scale bytes 4(lane%4).., d | dmin, code dwords

@@ -78,6 +78,12 @@ def main():
         out["q4_0_n16"] = _single(torch, G, dev, s, T.Q4_0, 11008, 4096, 16, 16)
     if "c1" in want:
         out["c1_f32"] = _single(torch, G, dev, s, T.F32, 512, 512, 512, 4)
+    if "down32" in want:
+        out["q4_0_4096x11008_n32"] = _single(torch, G, dev, s, T.Q4_0, 4096, 11008, 32, 16)
+    if "q80" in want:
+        out["q8_0_n32"] = _single(torch, G, dev, s, T.Q8_0, 11008, 4096, 32, 8)
+    if "q4k" in want:
+        out["q4_k_n32"] = _q4k(torch, G, dev, s, 11008, 4096, 32, 16)
     print(json.dumps(out), flush=True)
 
 
@@ -103,6 +109,32 @@ def _single(torch, G, dev, s, qt, M, K, N, copies):
     nbytes = nb + 4 * K * N + 4 * M * N
     del g
     return {"us": round(per * 1e6, 2), "frac": round(nbytes / per / 1e9 / 8000, 4),
+            "tflops": round(2 * M * N * K / per / 1e12, 1)}
+
+
+def _q4k(torch, G, dev, s, M, K, N, copies):
+    """Q4_K x F32 (bench.next_rows' synthetic super-blocks: random code bytes, d = 0.01, dmin = 0.001)."""
+    T = G.GGMLType
+    bb, so, _ = bench.KQ_BLOCK["Q4_K"]
+    nblk = M * K // 256
+    nb = nblk * bb
+    g = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+    wb, xb, db = g.addBuffer(copies * nb + 256), g.addBuffer(4 * K * N + 256), g.addBuffer(4 * M * N * copies + 256)
+    w = g.buffers[wb][: copies * nb].view(copies * nblk, bb)
+    w.copy_(torch.randint(0, 256, w.shape, dtype=torch.uint8, device=dev))
+    w[:, so:so + 4].copy_(torch.tensor([0.01, 0.001], dtype=torch.float16).view(torch.uint8).to(dev))
+    g.buffers[xb][: 4 * K * N].copy_(torch.randn(K * N, device=dev).view(torch.uint8))
+    nodes = [(G.GGMLTensor(T.Q4_K, [K, M], bufferId=wb, dataOffset=c * nb), G.GGMLTensor(T.F32, [N, K], bufferId=xb),
+              G.GGMLTensor(T.F32, [N, M], bufferId=db, dataOffset=4 * M * N * c)) for c in range(copies)]
+
+    def run_all():
+        for (a, b, d) in nodes:
+            G.computeMatMul(g, None, a, b, d, stream=s)
+
+    per, _ = bench._graph_time(torch, run_all, s, 10)
+    per /= copies
+    del g
+    return {"us": round(per * 1e6, 2), "frac": round((nb + 4 * K * N + 4 * M * N) / per / 1e9 / 8000, 4),
             "tflops": round(2 * M * N * K / per / 1e12, 1)}
 
 
