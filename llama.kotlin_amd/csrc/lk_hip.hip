@@ -398,10 +398,18 @@ GemmScratch &gemm_scratch() {
 // null — then splitk_reduce_kernel sums the slabs after the GEMM (LK_SKP_UNFUSED=1, one slice, slabs
 // beyond a 32-bit buffer offset, or more tiles per workgroup than its LDS list holds: list_ok false).
 // No co-residency is assumed: nobody waits, so any grid size and any concurrent stream are safe.
-int splitk_counters(int slices, size_t slab_bytes, int64_t ntiles, bool list_ok, unsigned **out) {
-  static const bool unfused = getenv("LK_SKP_UNFUSED") != nullptr;
+// Per-tile arrival counters for the in-launch split-K fix-up by the last arriver, or null: the slabs
+// are then summed by splitk_reduce_kernel launched after the GEMM (no waits either way). The default
+// is per kernel family (`in_launch`), measured round 4: the last arriver wins for the
+// wide kernel's two slices (C5 56.3 vs 56.2 µs: a launch saved at no cost) and loses for the skinny /
+// pair / sk kernels' eight (Q8_0 N = 32 36.9 vs 27.8 µs, Q4_K 35.3 vs 26.8, the down projection
+// 4096 x 11008 N = 32 on the pair kernel 43.7 vs 22.3): the slowest slice of a range ends up summing
+// every tile of it. LK_SKP_UNFUSED=1 / LK_SKP_FUSED=1 force either form (A/B).
+int splitk_counters(int slices, size_t slab_bytes, int64_t ntiles, bool list_ok, bool in_launch, unsigned **out) {
+  static const bool unfused = getenv("LK_SKP_UNFUSED") != nullptr, fused = getenv("LK_SKP_FUSED") != nullptr;
   *out = nullptr;
-  if (unfused || slices <= 1 || !list_ok || slab_bytes >= (1ull << 31) || ntiles <= 0) return LK_OK;
+  if (!fused && (unfused || !in_launch)) return LK_OK;
+  if (slices <= 1 || !list_ok || slab_bytes >= (1ull << 31) || ntiles <= 0) return LK_OK;
   GemmScratch &S = gemm_scratch();
   if (S.tcnt_n < (size_t)ntiles * kChainLine) {  // a 128-B line per tile
     const size_t want = std::max<size_t>((size_t)ntiles * kChainLine, 1 << 16);
@@ -572,7 +580,7 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
   const bool list_ok = 1 + (g.tiles_per_range + SG::NW - 1) / SG::NW <= SG::D * SG::SLOT / 4;  // a wave's ring
-  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, &rsync)) return rf;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, false, &rsync)) return rf;
   g.slices = slices;
   if (slices > 1) {
     const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
@@ -608,7 +616,7 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
   const bool list_ok = 1 + (g.tiles_per_range + 3) / 4 <= NT * 64 * 4;  // parity 0 of a pair's hand-off
-  if (int rc = splitk_counters(slices, slab_bytes, ntile, list_ok, &rsync)) return rc;
+  if (int rc = splitk_counters(slices, slab_bytes, ntile, list_ok, false, &rsync)) return rc;
   const bool fuse = rsync != nullptr;
   g.slices = slices;
   if (slices > 1) {
@@ -663,7 +671,7 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
   const bool list_ok = 1 + (g.tiles_per_range + 3) / 4 <= NT * 64 * 4;  // parity 0 of a pair's hand-off
-  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, &rsync)) return rf;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, false, &rsync)) return rf;
   g.slices = slices;
   if (slices > 1) {
     rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
@@ -731,7 +739,7 @@ int launch_kpart_t(const SkinnyArgs &s, hipStream_t st) {
     const size_t slab_bytes = (size_t)slices * g.M * 16 * NT * sizeof(float);
     if (int rc = grow(&S.partial, &S.partial_bytes, slab_bytes)) return rc;
     g.partial = (float *)S.partial;
-    if (int rc = splitk_counters(slices, slab_bytes, ntile, true, &g.tcnt)) return rc;
+    if (int rc = splitk_counters(slices, slab_bytes, ntile, true, false, &g.tcnt)) return rc;
   }
   g.tasks = ranges * slices;
   launch_xsplit(xa, st);
@@ -748,6 +756,7 @@ int launch_kpart_t(const SkinnyArgs &s, hipStream_t st) {
 
 int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   static const bool no_kpart = getenv_flag("LK_KPART_OFF");  // A/B: the round-3 skinny / pair kernels
+  static const bool kpart_all = getenv_flag("LK_KPART_ALL");  // A/B: every Q4 shape on the kpart kernel
   SkinnyArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
   g.b = (const uint8_t *)b->data + b->data_offset;
@@ -755,10 +764,14 @@ int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   g.dst = (uint8_t *)dst->data + dst->data_offset;
   g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
-  // Q4_0 / Q4_1 on the K-partitioned kernel (round 4); Q8_0 one wave per stream
+  // Q4_0 / Q4_1 at N <= 16 with at most two K slices (K <= 4096) on the K-partitioned kernel (round 4:
+  // the slices add into dst); otherwise the skinny / pair kernels with the slab reduce launch
+  // (measured round 4: N = 8 / 16 16.2 / 16.4 vs 17.5 / 17.7 µs; C3 N = 32 23.3 vs 23.0; the down
+  // projection 4096 x 11008 N = 32 28.5 vs 22.3). Q8_0 one wave per stream.
   const bool one = c.N <= 16;
-  if (!no_kpart && a->type == LK_TYPE_Q4_0) return one ? launch_kpart_t<LK_TYPE_Q4_0, 1>(g, st) : launch_kpart_t<LK_TYPE_Q4_0, 2>(g, st);
-  if (!no_kpart && a->type == LK_TYPE_Q4_1) return one ? launch_kpart_t<LK_TYPE_Q4_1, 1>(g, st) : launch_kpart_t<LK_TYPE_Q4_1, 2>(g, st);
+  const bool kp = !no_kpart && (kpart_all || (one && (c.K / 32 + 63) / 64 <= 2));
+  if (kp && a->type == LK_TYPE_Q4_0) return one ? launch_kpart_t<LK_TYPE_Q4_0, 1>(g, st) : launch_kpart_t<LK_TYPE_Q4_0, 2>(g, st);
+  if (kp && a->type == LK_TYPE_Q4_1) return one ? launch_kpart_t<LK_TYPE_Q4_1, 1>(g, st) : launch_kpart_t<LK_TYPE_Q4_1, 2>(g, st);
   switch (a->type) {
     case LK_TYPE_Q4_0: return one ? launch_skinny_t<LK_TYPE_Q4_0, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_0, 2>(g, st);
     case LK_TYPE_Q4_1: return one ? launch_skinny_t<LK_TYPE_Q4_1, 1>(g, st) : launch_skinny_pair_t<LK_TYPE_Q4_1, 2>(g, st);
@@ -819,7 +832,7 @@ int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
   g.tasks = nsuper * g.sm * g.sn * slices;
   // split-K fixed up inside gemm_wide_kernel by the last arriver per tile (splitk_counters)
   g.rsync = nullptr;
-  if (int rf = splitk_counters(slices, (size_t)slices * g.M * npad * sizeof(float), tiles, true, &g.rsync)) return rf;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * npad * sizeof(float), tiles, true, true, &g.rsync)) return rf;
   launch_xsplit(xa, st);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
