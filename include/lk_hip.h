@@ -191,9 +191,10 @@ int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor
  * then undefined) and re-arms the plan; 0 otherwise. Synchronizes the device. */
 int lk_plan_chain_timed_out(lk_plan *plan);
 void lk_plan_destroy(lk_plan *plan);
-/* Batched MUL_MATs (2 <= N) split K over workgroups and sum the slices inside the launch by the
- * LAST ARRIVER per output tile (round 4): nobody waits for another workgroup, so any grid size and
- * kernels of other streams sharing the GPU are safe. Only chain plans still wait (grid barriers,
+/* Batched MUL_MATs (2 <= N) split K over workgroups without any workgroup waiting for another
+ * (round 4): two slices add into dst, more store slabs summed by a reduce launch after the GEMM (or,
+ * in the wide kernel, by the LAST ARRIVER per output tile inside it), so any grid size and kernels of
+ * other streams sharing the GPU are safe. Only chain plans still wait (grid barriers,
  * every workgroup resident: one per CU). Such a wait is bounded (200 ms); one that gives up is
  * counted on the device and moves a per-device failure word: every synchronous entry point
  * (lk_mul_mat, lk_mul_mat_sharded, lk_graph_compute) reads the word before its launches and again

@@ -1,28 +1,28 @@
-// lk_kpart.hpp — gemm_kpart_kernel: Q4_0 / Q4_1 x F32 at 2 <= N <= 32 (config C3's batch 32), round 4.
+// lk_kpart.hpp — gemm_kpart_kernel: Q4_0 / Q4_1 x F32 at 2 <= N <= 16, K <= 4096 (round 4).
 //
 // computeMatMul's quantized dots (core/GGMLComputeOps.kt:70-145, dispatched at :1448-1480) for a few
 // activation columns, on v_mfma_f32_16x16x32_bf16, with the K dimension split INSIDE the workgroup.
 //
-// Why: the round-2/3 skinny kernels gave every workgroup one 16-block K slice (all of its waves hold
-// the same activations), so C3's K = 4096 took 8 workgroups per row range and 8 partial slabs per
-// output tile. Summing 8 slabs without waiting for the other workgroups (the last arriver does it,
-// round 4) cost C3 45 %. Here the 8 waves of a workgroup hold DIFFERENT K parts — wave w the
-// activation fragments of KB = 16/NT blocks (128 VGPRs: bf16 hi + lo, |x − hi − lo| ≤ 2⁻¹⁷|x|, split
-// once per call by xsplit_kernel and loaded as coalesced 16-B pieces) — so a workgroup covers 8·KB
-// blocks (64 at N = 32: K = 2048) and C3 needs 2 slices, 11008 6; at N <= 16 a workgroup spans
-// K = 4096 whole (no slabs at all).
+// Why: the round-2/3 skinny kernels give every workgroup one 16-block K slice (all of its waves hold
+// the same activations), so K = 4096 takes 8 workgroups per row range and 8 partial slabs per output
+// tile, which round 3 summed by making the slices wait for each other inside the launch. Here the 8
+// waves of a workgroup hold DIFFERENT K parts — wave w the activation fragments of KB = 8 blocks
+// (64·NT VGPRs: bf16 hi + lo, |x − hi − lo| ≤ 2⁻¹⁷|x|, split once per call by xsplit_kernel and
+// loaded as coalesced 16-B pieces) — so a workgroup covers 64 blocks (K = 2048) and K = 4096 is two
+// slices, which add their tile sums into dst (zeroed by the xsplit launch): two addends per element,
+// so the order cannot change a bit, and no workgroup waits for another. More slices (K > 4096, only
+// with LK_KPART_ALL) store slabs summed by the last arriver per tile or by splitk_reduce_kernel.
+// The product routes N <= 16 here (measured round 4: N = 8 / 16 16.0 / 16.3 µs against 17.5 / 17.7
+// on the skinny kernel with the reduce launch); at N = 32 the pair kernel with the reduce launch is
+// as fast (C3 23.0 vs 23.3 µs) and the down projection (K = 11008, six slices) much faster.
 //
 // Schedule: workgroup = (row range, K slice); each wave streams every 16-row tile of the range
 // through its own LDS-DMA ring (its row pieces: KB blocks of 16 rows, nt policy), computes its
 // partial 16 x 16·NT tile (codes as bf16 — Q4_0 the exact 128 + n, Q4_1 n·2⁻⁹ — against its held
 // fragments, the block scale after each block's MFMA pair, the per-block offset term on the f32
-// MFMA once per unit), writes it to an LDS slot of the tile and counts itself in with an LDS atomic:
-// the wave whose count completes the tile sums the 8 partials in wave order (deterministic) and
-// stores the tile — into dst when the workgroup spans all of K, else as this slice's partial slab
-// (write-through). At the end each wave arrives on the counters of the tiles it stored; the last
-// slice to arrive sums the tile's slabs in slice order: nobody waits for another workgroup (and no
-// workgroup barrier is needed). Inside the workgroup a wave may run at most NB tiles ahead of the
-// slowest (LDS slots).
+// MFMA once per unit), writes it to an LDS slot of the tile (row-major rows) and counts itself in;
+// the tile's owner (the wave of part tile % active parts) sums the partials in part order two units
+// later. Inside the workgroup a wave may run at most NB tiles ahead of the slowest (LDS slots).
 #pragma once
 
 #include "lk_kernels.hpp"
