@@ -1640,10 +1640,19 @@ __device__ __forceinline__ void splitk_tiles_fixup(unsigned *tcnt, const __amdgp
   }
 }
 
-// a partial slab's f32x4: write-through when the reduction is fused (another workgroup reads it)
-__device__ __forceinline__ void store_partial(bool fused, const __amdgpu_buffer_rsrc_t prs, float *partial, int64_t idx,
+// a partial slab's f32x4, written through (sc1) whenever the slab fits a buffer resource: another
+// workgroup of the launch (the last arriver) or the reduce launch after it reads it, and a plain
+// store would leave the line dirty in this XCD's L2 — written back at the kernel boundary, which
+// costs that boundary ~1 µs per 6 MB (MI355X_MICROARCH.md, boundary; C3's slabs are 11 MB)
+#ifndef LK_SLAB_PLAIN
+#define LK_SLAB_PLAIN 0  // lab builds only: plain slab stores when the reduction is a separate launch
+#endif
+__device__ __forceinline__ bool slab_wt(bool fused, int64_t slab_bytes) {
+  return fused || (!LK_SLAB_PLAIN && slab_bytes < (1ll << 31));
+}
+__device__ __forceinline__ void store_partial(bool wt, const __amdgpu_buffer_rsrc_t prs, float *partial, int64_t idx,
                                               f32x4 v) {
-  if (fused) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), prs, (int)(idx * 4), 0, 16);
+  if (wt) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), prs, (int)(idx * 4), 0, 16);
   else *(f32x4 *)(partial + idx) = v;
 }
 
@@ -1762,7 +1771,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
 
   const int N16 = 16 * NT;
   const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, slab_wt(g.rsync != nullptr, (int64_t)g.slices * g.M * N16 * 4) ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
   int slot = 0;
   for (int u = 0; u < nunits; u++) {
     // ops younger than unit u's DMA (issue order: units 0..D-1 in the prologue, then per tile
@@ -1793,7 +1802,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
     for (int j = 0; j < NT; j++) {
       const int n0 = 16 * j + 4 * (lane >> 4);
       if (g.slices > 1) {
-        if (m < g.M) store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, acc[j]);
+        if (m < g.M) store_partial(slab_wt(g.rsync != nullptr, (int64_t)g.slices * g.M * N16 * 4), prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, acc[j]);
       } else if (m < g.M) {
         const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
 #pragma unroll
@@ -2053,7 +2062,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   const int N16 = 16 * NT;
   // the partial slabs as a buffer (fused reduction: sc1 stores and loads; the host checks the size)
   const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, slab_wt(g.rsync != nullptr, (int64_t)g.slices * g.M * N16 * 4) ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
   const int SH = h == 0 ? NT : 0;  // stores per unit (at least; slices == 1 may store more)
   [[maybe_unused]] const uint64_t t_loop = LK_KP_T();
   for (int u = 0; u < nunits; u++) {
@@ -2115,7 +2124,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       for (int j = 0; j < NT; j++) {
         const int n0 = 16 * j + 4 * (lane >> 4);
         if (g.slices > 1) {
-          if (m < g.M) store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, acc[j]);
+          if (m < g.M) store_partial(slab_wt(g.rsync != nullptr, (int64_t)g.slices * g.M * N16 * 4), prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, acc[j]);
         } else if (m < g.M) {
           const float e4[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
 #pragma unroll
@@ -2423,7 +2432,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
   __syncthreads();
   const int npad = g.tiles_n * BN;
   const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * npad * 4 : 0, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, slab_wt(g.rsync != nullptr, (int64_t)g.slices * g.M * npad * 4) ? g.slices * g.M * npad * 4 : 0, 0x00020000);
   auto store_dst = [&](int64_t m, int n0, const f32x4 &v) __attribute__((always_inline)) {
     const float e4[4] = {v.x, v.y, v.z, v.w};
     if (g.d_nb0 == 4 && n0 + 4 <= g.N && ((((uintptr_t)g.dst + m * g.d_nb1 + n0 * 4) & 15) == 0)) {
@@ -2450,7 +2459,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
 #pragma unroll
       for (int j = 0; j < NT; j++) {
         const int n0 = tn * BN + j * 16 + 4 * (lane >> 4);
-        if (g.slices > 1) store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * npad + n0, acc[i][j]);
+        if (g.slices > 1) store_partial(slab_wt(g.rsync != nullptr, (int64_t)g.slices * g.M * npad * 4), prs, g.partial, ((int64_t)slice * g.M + m) * npad + n0, acc[i][j]);
         else store_dst(m, n0, acc[i][j]);
       }
     }

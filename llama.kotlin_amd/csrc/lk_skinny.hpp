@@ -377,7 +377,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 
   const int N16 = 16 * NT;
   const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, g.rsync ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, slab_wt(g.rsync != nullptr, (int64_t)g.slices * g.M * N16 * 4) ? g.slices * g.M * N16 * 4 : 0, 0x00020000);
   // h = 0 collects unit u − 1's partner sums after computing unit u (the partner, at higher issue
   // priority, is ahead), so neither wave idles while the other computes: the two waves of a SIMD
   // overlap their VALU / MFMA streams.
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     for (int j = 0; j < NT; j++) {
       const int n0 = 16 * j + 4 * (lane >> 4);
       if (g.slices > 1) {
-        if (m < g.M) store_partial(g.rsync != nullptr, prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, sum[j]);
+        if (m < g.M) store_partial(slab_wt(g.rsync != nullptr, (int64_t)g.slices * g.M * N16 * 4), prs, g.partial, ((int64_t)slice * g.M + m) * N16 + n0, sum[j]);
       } else if (m < g.M) {
         const float e4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
 #pragma unroll
