@@ -331,7 +331,8 @@ int cu_count() {
 template <int QT, int CPL>
 void launch_stream_t(int grid, const GemvDesc &single, const StreamWork *work, int spw, hipStream_t st) {
   constexpr size_t lds = StreamGeom<QT, CPL>::LDS;
-  hipLaunchKernelGGL((gemv_stream_kernel<QT, CPL>), dim3(grid), dim3(kStreamWaves * 64), lds, st, single, work, spw);
+  hipLaunchKernelGGL((gemv_stream_kernel<QT, CPL>), dim3(grid), dim3(kStreamWaves * 64), lds, st, work, spw, single.a, single.x,
+                     single.dst, single.dst_row_stride, single.M, single.K);
 }
 
 int launch_stream(int32_t qt, int cpl, int grid, const GemvDesc &single, const StreamWork *work, int spw,

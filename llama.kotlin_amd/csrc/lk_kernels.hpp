@@ -453,16 +453,19 @@ __device__ float q2k_stream_dot(uint32_t sc, const uint32_t *c, uint32_t dd, con
 // [wg0, wg0 + nwg) per node, rows split evenly over them); otherwise workgroup g runs its slots
 // of args.work (chain plans).
 // Requirements (checked by the host): K % 64 == 0, ceil(K/4096) <= CPL, row bytes
-// (K/64·PB) % 16 == 0, A and x 16-byte aligned, x contiguous.
+// (K/64·PB) % 16 == 0, A and x 16-byte aligned, x contiguous. Scalar arguments only (no
+// aggregate), the work list first, so the compiler can preload them into SGPRs.
 template <int QT, int CPL>
-__global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const GemvDesc single,
-                                                                        const StreamWork *__restrict__ work, int spw) {
+__global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const StreamWork *__restrict__ work, int spw,
+                                                                        const uint8_t *s_a, const float *s_x, float *s_dst,
+                                                                        int64_t s_dst_stride, int s_M, int s_K) {
   using G = StreamGeom<QT, CPL>;
   extern __shared__ f32x4 lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   [[maybe_unused]] const uint64_t t_entry = LK_KP_T();
   [[maybe_unused]] int st_units = 0;
+  [[maybe_unused]] uint64_t t_rec = 0, t_iss = 0, t_img = 0, t_x = 0, t_u0 = 0;  // lab stamps (first segment)
   uint8_t *ring = (uint8_t *)lds + G::IMG + wave * (G::D * G::SLOT);
   float *q63 = (float *)((uint8_t *)lds + G::TOFF);  // K-quants only; published by the prologue's barrier
   if constexpr (QT == LK_TYPE_Q4_K)
@@ -492,11 +495,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       K = w.K; rb = w.row_begin; re = w.row_end;
       bar = w.barrier; nbar = w.nbar; sync = w.sync;
     } else {
-      a_node = single.a; x_node = single.x; dst_node = single.dst; dst_stride = single.dst_row_stride;
-      K = single.K;
-      const int per = (single.M + (int)gridDim.x - 1) / (int)gridDim.x;
-      rb = min((int)blockIdx.x * per, single.M);
-      re = min(rb + per, single.M);
+      a_node = s_a; x_node = s_x; dst_node = s_dst; dst_stride = s_dst_stride;
+      K = s_K;
+      const int per = (s_M + (int)gridDim.x - 1) / (int)gridDim.x;
+      rb = min((int)blockIdx.x * per, s_M);
+      re = min(rb + per, s_M);
     }
     const int NP = K >> 6;                         // block pairs per row
     const int nch = (NP + 63) >> 6;                // units per row
@@ -506,6 +509,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + per_w, re) - r0);
     const int nunits = nrows * nch;
     st_units += nunits;
+#ifdef LK_LAB_STAMPS
+    asm volatile("" ::"s"(nunits));
+    if (si == 0) t_rec = LK_KP_T();
+#endif
     const LK_GLOBAL uint8_t *A = (const LK_GLOBAL uint8_t *)a_node + (int64_t)r0 * RB;
 
     // 1. prologue, all by LDS-DMA:
@@ -650,8 +657,14 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     if (si > 0) __builtin_amdgcn_s_barrier();  // every wave is done with the previous segment's image
     dma_x();
     weight_prologue();
+#ifdef LK_LAB_STAMPS
+    if (si == 0) t_iss = LK_KP_T();
+#endif
     wait_vmcnt<G::D * G::L>();     // this wave's activation DMA has landed
     __builtin_amdgcn_s_barrier();  // ... and every other wave's
+#ifdef LK_LAB_STAMPS
+    if (si == 0) t_img = LK_KP_T();
+#endif
     }
 
     // 2. activations into VGPRs in decode order, and Σx per block (only the node's own chunks:
@@ -707,6 +720,10 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
       }
     }
 
+#ifdef LK_LAB_STAMPS
+    asm volatile("" ::"v"(xs0[0]), "v"(xs1[0]));
+    if (si == 0) t_x = LK_KP_T();
+#endif
     int slot = 0, u = 0;
     LK_GLOBAL float *out = (LK_GLOBAL float *)dst_node + (int64_t)r0 * dst_stride;
     for (int row = 0; row < nrows; row++) {
@@ -722,6 +739,9 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
           else __builtin_amdgcn_s_setprio(0);
           if (u + G::D - 1 < nunits) wait_vmcnt<G::VMCNT>();  // a full ring: D − 1 units issued past unit u
           else wait_vmcnt<0>();
+#ifdef LK_LAB_STAMPS
+          if (si == 0 && u == 0) t_u0 = LK_KP_T();
+#endif
           const uint32_t *rp = (const uint32_t *)(ring + slot * G::SLOT + lane * G::PB);
           uint32_t w[G::PDW];
           u32x4 kh, kc0, kc1;  // Q4_K: block lane/4's header and sub-blocks 2(lane%4), +1
@@ -762,6 +782,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const Ge
     }
   }
   LK_KP_SET(0, t_entry); LK_KP_SET(4, LK_KP_T()); LK_KP_SET(8, (uint64_t)st_units);
+  LK_KP_SET(1, t_rec); LK_KP_SET(2, t_iss); LK_KP_SET(3, t_img); LK_KP_SET(5, t_x); LK_KP_SET(6, t_u0);
   if (sync) {
     // chain plans: the workgroup that leaves last (every workgroup has passed every barrier)
     // re-arms the counters for the next launch (stream order makes the stores visible to it)

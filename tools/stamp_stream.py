@@ -47,6 +47,16 @@ def main():
         entry = np.array([(st[w, live[w], 0].min() - t0) / 100 for w in wgs])
         exit_ = np.array([(st[w, live[w], 4].max() - t0) / 100 for w in wgs])
         units = np.array([st[w, live[w], 8].max() for w in wgs])
+        # per-wave phases (slots 1-3, 5, 6 of the stream kernel's lab build): median over waves,
+        # µs after the earliest entry and after the wave's own entry
+        names = {1: "record", 2: "dma_issued", 3: "image_barrier", 5: "x_in_vgprs", 6: "unit0_landed", 4: "exit"}
+        ph, ph_own = {}, {}
+        wl = st[live]
+        for i, nm in names.items():
+            ok = wl[:, i] > 0
+            ph[nm] = round(float(np.median((wl[ok, i] - t0) / 100)), 2)
+            ph_own[nm] = round(float(np.median((wl[ok, i] - wl[ok, 0]) / 100)), 2)
+        ph["entry"] = round(float(np.median((wl[:, 0] - t0) / 100)), 2)
         grp = 16
         out[f"rep{rep}"] = {
             "workgroups": int(len(wgs)),
@@ -54,7 +64,7 @@ def main():
             "exit_by_group": [round(float(np.median(exit_[i:i + grp])), 2) for i in range(0, len(wgs), grp)],
             "exit_max": round(float(exit_.max()), 2), "exit_med": round(float(np.median(exit_)), 2),
             "entry_by_xcd": [round(float(np.median(entry[x::8])), 2) for x in range(8)],
-            "units_per_wave_max": int(units.max())}
+            "units_per_wave_max": int(units.max()), "phases_from_first_entry": ph, "phases_from_own_entry": ph_own}
     print(json.dumps(out), flush=True)
 
 
