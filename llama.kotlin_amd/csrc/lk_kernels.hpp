@@ -517,7 +517,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const St
 
     // 1. prologue, all by LDS-DMA:
     //    - weights: exactly D units in flight; past the wave's last unit (or for a wave
-    //      without rows) the slots are filled from the node's first 16 bytes and never decoded;
+    //      without rows) the slots are filled from the node's first row and never decoded;
     //    - the activation image: float4 t (x[4t..4t+3]) of pair p at lds[16p + (t ^ (p & 15))]
     //      (XOR swizzle: each DMA instruction reads 1 KB of x contiguously, and the per-lane
     //      reads below hit 64 distinct banks); image float4 i = 64·k + lane comes from DMA
@@ -589,9 +589,7 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const St
       for (int k = 0; k < G::D; k++) {
         const bool real = k < nunits;
         const LK_GLOBAL uint8_t *base = real ? A + (int64_t)irow * RB + (int64_t)ich * G::UB : (const LK_GLOBAL uint8_t *)a_node;
-        // a filler (never decoded) has every lane read the node's first 16 bytes: one cache line per
-        // instruction for the address path instead of sixteen, the same DMA count for the waits
-        const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : 0;
+        const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : (int)min((int64_t)G::UB, RB);
         dma_unit(base, ubytes, k);
         if (real) {
           advance();
