@@ -2184,7 +2184,7 @@ int graph_build(lk_comm *comm, const lk_tensor *a, const lk_tensor *b, const lk_
     // (never on a sharded graph: its all-gathers write the dst mirrors)
     r.direct = !g_no_direct && !comm && hits(down_m, s) && !hits(reads, s) && !hits(up_m, s);
     const uint64_t skew = (s.host + s.lo) & 255;
-    const hipError_t e = r.direct ? hipHostMalloc(&r.alloc, s.hi - s.lo + skew, hipHostMallocCoherent)
+    const hipError_t e = r.direct ? hipHostMalloc(&r.alloc, s.hi - s.lo + skew, hipHostMallocDefault)
                                   : hipMalloc(&r.alloc, s.hi - s.lo + skew);
     if (e != hipSuccess) {
       lk_graph_destroy(g);
