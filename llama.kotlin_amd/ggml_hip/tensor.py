@@ -302,6 +302,9 @@ class GGMLGraphAllocator:
             # bytes, so its mirrors are evicted with it.
             if buf.size:
                 weakref.finalize(buf, _evict_host_buffer, int(buf.ctypes.data), int(buf.size))
+                # ... and a new ByteArray supersedes whatever mirrors still cover its address (an
+                # earlier buffer's eviction can run late, e.g. when a graph object held it in a cycle)
+                _evict_host_buffer(int(buf.ctypes.data), int(buf.size))
             return buf
         import torch
         return torch.zeros(max(nbytes, 0), dtype=torch.uint8, device=self.device)
