@@ -23,6 +23,12 @@ C-ABI communicator is built from a world-1 NCCL process group and each layer is 
 lk_sharded_plan with its RCCL group of in-place gathers, captured in the HIP graph — the exact
 code the 8-GPU run executes, measured on one GPU (its value should match the plain line).
 
+Launching N ranks: under torchrun (WORLD_SIZE set) every rank is one process on GPU LOCAL_RANK and
+`--gpus`, when given, must equal WORLD_SIZE. Run directly with `--gpus N > 1`, bench.py starts the N
+rank processes itself before anything touches a GPU (torchrun's environment per rank, rendezvous on
+127.0.0.1), relays rank 0's JSON line and exits with the worst rank's status. It refuses (exit 2) a
+`--gpus` that disagrees with WORLD_SIZE or exceeds the visible GPUs (the gloo rehearsal excepted).
+
 Exit status: the JSON line is always printed; the run exits 3 afterwards when any section reports
 an error or any bounded in-launch wait gave up (sync_wait_timeouts), so a driver never takes a
 partial line for a clean one.
@@ -79,9 +85,45 @@ def capture(torch, fn, stream):
     return g
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """Start n rank processes of this script (torchrun's per-rank environment, rendezvous on
+    127.0.0.1) before any GPU call in this process; rank 0's stdout is the caller's. Returns the
+    worst exit status; when a rank fails the others are stopped (they would wait at a barrier)."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LK_BENCH_SPAWNED="1")
+        out = None if r == 0 else subprocess.DEVNULL  # only rank 0 prints the line
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, stdout=out))
+    worst = 0
+    while procs:
+        for p in list(procs):
+            rc = p.poll()
+            if rc is None:
+                continue
+            procs.remove(p)
+            if rc != 0:
+                worst = worst or rc
+                for q in procs:  # a failed rank leaves the others waiting for it
+                    q.terminate()
+        time.sleep(0.05)
+    return worst
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, or 1)")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="start the ranks, join the process group, report what each rank sees, exit (no GPU work)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layers", type=int, default=LAYERS)
@@ -100,12 +142,39 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # LK_BENCH_BACKEND=gloo (rehearsal only, never a measurement): the N > 1 code path with
     # ranks sharing the visible GPUs and gloo collectives, to exercise it on a one-GPU box
     backend = os.environ.get("LK_BENCH_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ:
+        n = args.gpus or 1
+        # (torch.cuda.device_count() does not initialise the GPU on this image: safe before the fork)
+        if n > 1 and backend == "nccl" and not args.check_launch and torch.cuda.device_count() < n:
+            print(f"[bench] --gpus {n}: only {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+            sys.exit(2)
+        if n > 1:
+            sys.exit(spawn_ranks(n, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing a line that would misstate n_gpus",
+              file=sys.stderr)
+        sys.exit(2)
+    if args.check_launch:  # launcher check: no GPU work (CPU tests run it with the gloo backend)
+        if world > 1:
+            dist.init_process_group("gloo")
+            seen = dist.get_world_size()
+            dist.barrier()
+            dist.destroy_process_group()
+        else:
+            seen = 1
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "ranks_seen": seen, "spawned": os.environ.get("LK_BENCH_SPAWNED") == "1",
+                              "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
+    if backend == "nccl" and torch.cuda.device_count() < world:
+        print(f"[bench] WORLD_SIZE={world} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+        sys.exit(2)
     if backend != "nccl":
         local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
@@ -170,6 +239,8 @@ def main():
     if distributed and backend == "nccl":
         # the C-ABI's RCCL path is the product: if it cannot be set up the run fails (no fallback)
         comm = G.Comm.from_process_group()
+        if comm.rcclRanks != world:
+            raise SystemExit(f"RCCL communicator holds {comm.rcclRanks} ranks, WORLD_SIZE is {world}")
         plans = [[G.ShardedMulMatPlan(comm, ga, [n[name] for (name, _, _) in LAYER_MATS])] for n in nodes_by_layer]
     elif world > 1:  # LK_BENCH_BACKEND=gloo rehearsal only: local launch + torch.distributed gather
         plans = [[G.MulMatPlan(ga, lp)] for lp in local_by_layer]
@@ -235,11 +306,27 @@ def main():
 
     roof = roofline(torch, local_plans, local_by_layer, compute, world)
 
+    # the decode figure: the dependent order {q,k,v} -> o -> {gate,up} -> down (4 launches per layer;
+    # at N > 1 each a sharded plan with its all-gather), timed on every rank, max over ranks
+    decode = None
+    if not args.no_chain and not (world > 1 and comm is None):
+        try:
+            if comm is not None:
+                mk = lambda nodes: G.ShardedMulMatPlan(comm, ga, nodes)  # noqa: E731
+            else:
+                mk = lambda nodes: G.MulMatPlan(ga, nodes)  # noqa: E731
+            decode = decode_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, make_plan=mk,
+                                  dist=dist if distributed else None, dev=dev)
+        except G.HipDeviceError as e:
+            decode = {"error": str(e)}
+
     result = {
         "metric": "Q4_0 matmul GB/s + tokens/sec 7B, 1/2/4/8 MI355X vs Kotlin CPU",
         "value": round(value_gbs, 2),
         "unit": "GB/s",
-        "tokens_per_s": round(tokens / elapsed, 2),
+        # tokens/s of the dependent decode order (decode_chain); the timed grouped step's own rate beside it
+        "tokens_per_s": decode.get("tokens_per_s") if isinstance(decode, dict) else None,
+        "tokens_per_s_grouped_step": round(tokens / elapsed, 2),
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -258,6 +345,7 @@ def main():
                    "parallelism": (f"row-shard{world}+{'rccl-c-abi' if comm is not None else 'torch-' + backend}-allgather"
                                    if distributed else "single"),
                    "launches_per_step_per_rank": launches_per_step, "hip_graph": graph is not None,
+                   "ranks_seen_by_rccl": comm.rcclRanks if comm is not None else None,
                    "gpu_ms_per_step": round(ev_ms / args.steps, 4)},
         "roofline": roof,
     }
@@ -277,8 +365,9 @@ def main():
             result[key] = {"error": str(e)}
         waits[key] = G.syncTimeouts()
 
+    if decode is not None:
+        result["decode_chain"] = decode
     if rank == 0 and world == 1 and not args.no_chain:
-        section("decode_chain", lambda: decode_chain(torch, G, ga, nodes_by_layer, compute, token_bytes))
         section("persistent_chain", lambda: {
             "layer_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 1),
             "decode_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 4)})
@@ -370,10 +459,14 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def decode_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, reps=20):
-    """Dependent decode schedule on one GPU: per layer {q,k,v} -> o -> {gate,up} -> down,
-    4 stream-ordered launches (128 per token), captured in a HIP graph."""
-    plans = [[G.MulMatPlan(ga, [n[k] for k in grp]) for grp in CHAIN] for n in nodes_by_layer]
+def decode_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, reps=20, make_plan=None, dist=None, dev=None):
+    """Dependent decode schedule: per layer {q,k,v} -> o -> {gate,up} -> down, 4 stream-ordered
+    launches (128 per token), captured in a HIP graph. make_plan builds one group's plan (N = 1: a
+    MulMatPlan; N > 1: a ShardedMulMatPlan, its in-place all-gather after the launch). With dist,
+    every rank times the token and the max over ranks is reported."""
+    if make_plan is None:
+        make_plan = lambda nodes: G.MulMatPlan(ga, nodes)  # noqa: E731
+    plans = [[make_plan([n[k] for k in grp]) for grp in CHAIN] for n in nodes_by_layer]
 
     def token():
         for lp in plans:
@@ -394,9 +487,18 @@ def decode_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, reps=20):
         e1.record(stream)
     torch.cuda.synchronize()
     per = e0.elapsed_time(e1) / 1e3 / reps
+    if dist is not None:
+        t = torch.tensor([per], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        per = float(t.item())
+    for lp in plans:
+        for p in lp:
+            p.close()
     return {"tokens_per_s": round(1 / per, 2), "ms_per_token": round(per * 1e3, 4),
             "achieved_GBps": round(token_bytes / per / 1e9, 1), "launches_per_token": 4 * len(plans),
-            "hip_graph": g is not None, "tokens_timed": reps}
+            "hip_graph": g is not None, "tokens_timed": reps,
+            "schedule": "{q,k,v} -> o -> {gate,up} -> down per layer" + (", each group a row-sharded plan + RCCL all-gather"
+                                                                        if dist is not None else "")}
 
 
 def persistent_chain(torch, G, ga, nodes_by_layer, stream, token_bytes, per_layer, reps=20):

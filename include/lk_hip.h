@@ -166,6 +166,9 @@ int lk_mul_mat_device(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, vo
  * one wave's sequential sum). Falls back to one device when rows are not byte
  * ranges (quantized A with K % 32 != 0) or dst rows interleave. Synchronous. */
 int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, int n_shards);
+/* The same with shard r on device (first_device + r) mod lk_device_count() (a backend bound to
+ * GPU first_device; lk_mul_mat_sharded is first_device = 0). */
+int lk_mul_mat_sharded_at(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, int n_shards, int first_device);
 
 /* ---- grouped execution of independent MUL_MAT nodes ------------------------ */
 
@@ -212,6 +215,16 @@ int lk_sync_timeouts(uint32_t *count);
  *   launches (the last arrival of each tile re-arms its word). */
 int lk_set_sync_wait_bound(uint64_t ticks);
 int lk_sync_counters_sum(uint64_t *sum);
+/* Diagnostic (no reference counterpart): the kernels the calls on this thread launched since the
+ * last lk_debug_route_clear, and for lk_mul_mat where A came from ("A=mirror" / "A=staged"), as
+ * space-separated words, e.g. "A=mirror gemm_q_mfma<2>:t2s12". Lets a parity test name the route
+ * that produced a result. */
+const char *lk_debug_route(void);
+void lk_debug_route_clear(void);
+/* Diagnostic: how many times the batched kernels' device scratch (activation fragments, split-K
+ * slabs, tile counters) of the current device was reallocated. Outgrown buffers are retired, never
+ * freed before lk_shutdown, so HIP graphs captured earlier stay valid. */
+uint64_t lk_debug_scratch_epoch(void);
 
 /* ---- multi-GPU: row shards + RCCL all-gather over xGMI -----------------
  * The reference is single-device; this is the north star's partition of the same operator.
@@ -360,6 +373,7 @@ uint64_t lk_weights_cached_count(void);
 /* Pin each row shard of a quantized A on the device lk_mul_mat_sharded(…, n_shards)
  * runs it on (the mirror lk_weights_pin keeps, per shard and device). */
 int lk_weights_pin_sharded(const lk_tensor *a, uint64_t generation, int n_shards);
+int lk_weights_pin_sharded_at(const lk_tensor *a, uint64_t generation, int n_shards, int first_device);
 
 /* ---- format kernels (the steps either side of the path) --------------------- */
 

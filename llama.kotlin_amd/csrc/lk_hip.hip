@@ -32,6 +32,19 @@ using namespace lk;
 namespace {
 
 thread_local std::string g_err;
+thread_local std::string g_route;  // lk_debug_route: kernels launched on this thread since the last clear
+
+void note_route(const char *fmt, ...) {
+  char buf[160];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (g_route.size() < 4096) {
+    if (!g_route.empty()) g_route += ' ';
+    g_route += buf;
+  }
+}
 
 int fail(int st, const char *fmt, ...) {
   char buf[512];
@@ -60,6 +73,11 @@ namespace {
 // residency cache and staging scratch. lk_mul_mat uses the current device;
 // lk_mul_mat_sharded drives several from one host thread.
 constexpr int kMaxDevices = 64;
+
+// Device copies of A (weight mirrors, the host path's staging) carry this many bytes past the
+// matrix: the wide and LDS GEMMs' last row windows read up to OVERREAD (< 64) bytes beyond it, and
+// they take a matrix only when those bytes are inside its buffer (wide_eligible, gemm_lds_eligible).
+constexpr uint64_t kASlack = 256;
 
 // A device mirror of host bytes [lo, lo + bytes) of the ByteArray at `base`, as of weight
 // generation `gen`. Shared: the cache holds one reference while the mirror is current, every
@@ -338,6 +356,7 @@ void launch_stream_t(int grid, const GemvDesc &single, const StreamWork *work, i
 int launch_stream(int32_t qt, int cpl, int grid, const GemvDesc &single, const StreamWork *work, int spw,
                   hipStream_t st) {
   if (grid <= 0) return LK_OK;
+  note_route("stream<%d,%d>:g%d%s", qt, cpl, grid, work ? "p" : "");
 #define LK_STREAM(T, C) \
   if (qt == T && cpl == C) { launch_stream_t<T, C>(grid, single, work, spw, st); HIP_TRY(hipGetLastError()); return LK_OK; }
   LK_STREAM(LK_TYPE_Q4_0, 1) LK_STREAM(LK_TYPE_Q4_0, 2) LK_STREAM(LK_TYPE_Q4_0, 3)
@@ -361,6 +380,7 @@ int launch_gemv_v1(int32_t qt, const GemvDesc &d, hipStream_t st) {
   if (ntiles <= 0) return LK_OK;
   if (ntiles > INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "too many rows");
   dim3 grid((unsigned)ntiles), block(256);
+  note_route("gemv_v1<%d>", qt);
   switch (qt) {
     case LK_TYPE_Q4_0: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q4_0, kRowsQ4>), grid, block, 0, st, d); break;
     case LK_TYPE_Q4_1: hipLaunchKernelGGL((gemv_q_n1_kernel<LK_TYPE_Q4_1, kRowsQ4>), grid, block, 0, st, d); break;
@@ -378,21 +398,64 @@ bool gemm_eligible(const Checked &c) {
 }
 
 // Device scratch for the GEMM (activation fragments, block sums, split-K partials, tile
-// counters), per device, grow-only. Allocated outside any capture on first use; counters are
-// zeroed once and re-armed by the kernel.
+// counters), per device and stream (gemm_scratch), grow-only. Counters are zeroed when allocated — on the launch's stream
+// (hipMemsetAsync: stream-ordered before the launch that first uses them, and part of a capture
+// that allocates them) — and re-armed by the kernels.
+//
+// Lifetime: launches captured into HIP graphs (lk_graph's replay, a caller's torch / HIP graph of
+// lk_mul_mat_device or lk_plan_launch) bake these pointers in. A buffer outgrown by a later call is
+// therefore never freed while the library lives: it is retired (kept allocated, untouched by any new
+// launch) and released by lk_shutdown, so a replay captured before the growth still reads and writes
+// memory that belongs to it. Growth doubles, so the retired bytes stay below the live ones.
+// `epoch` counts reallocations (lk_graph records it; diagnostic).
 struct GemmScratch {
   void *frag = nullptr; size_t frag_bytes = 0;
   void *partial = nullptr; size_t partial_bytes = 0;
   int32_t *counter = nullptr; size_t counter_n = 0;
   unsigned *tcnt = nullptr;  // split-K arrival counters, one word per output tile of a launch
   size_t tcnt_n = 0;
+  std::vector<void *> retired;
+  uint64_t epoch = 0;
 };
 
-GemmScratch &gemm_scratch() {
-  static GemmScratch per_dev[64];
+// One scratch per (device, stream): launches on different streams never share fragments, slabs or
+// counters, so two streams may run batched MUL_MATs concurrently (a torch side stream and the
+// library stream of the host path, say). A stream handle reused after hipStreamDestroy inherits the
+// old stream's scratch, which its work no longer touches.
+struct ScratchKey {
+  int dev;
+  hipStream_t st;
+  bool operator<(const ScratchKey &o) const { return dev != o.dev ? dev < o.dev : (uintptr_t)st < (uintptr_t)o.st; }
+};
+std::mutex g_scratch_mu;
+std::map<ScratchKey, GemmScratch> &scratch_map() {
+  static std::map<ScratchKey, GemmScratch> m;  // node-based: references stay valid as it grows
+  return m;
+}
+
+GemmScratch &gemm_scratch(hipStream_t st) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  return per_dev[dev];
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  return scratch_map()[ScratchKey{dev, st}];
+}
+
+// Grow *p to at least `want` bytes (at least double the old size); the old buffer is retired, not
+// freed (see GemmScratch). zero: zero the new bytes on stream st (counters).
+int grow_scratch(GemmScratch &S, void **p, size_t *have, size_t want, bool zero, hipStream_t st) {
+  if (*have >= want) return LK_OK;
+  const size_t bytes = std::max(want, 2 * *have);
+  void *q = nullptr;
+  if (hipMalloc(&q, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(LK_ERR_DEVICE, "scratch: hipMalloc of %zu B failed", bytes);
+  }
+  if (zero) HIP_TRY(hipMemsetAsync(q, 0, bytes, st));
+  if (*p) S.retired.push_back(*p);
+  *p = q;
+  *have = bytes;
+  S.epoch++;
+  return LK_OK;
 }
 // Split-K fix-up by the last arriver (lk_kernels.hpp splitk_arrive): the per-tile arrival counters
 // to pass (ntiles words, zero between launches: the last arrival of each tile re-arms its word), or
@@ -406,22 +469,36 @@ GemmScratch &gemm_scratch() {
 // pair / sk kernels' eight (Q8_0 N = 32 36.9 vs 27.8 µs, Q4_K 35.3 vs 26.8, the down projection
 // 4096 x 11008 N = 32 on the pair kernel 43.7 vs 22.3): the slowest slice of a range ends up summing
 // every tile of it. LK_SKP_UNFUSED=1 / LK_SKP_FUSED=1 force either form (A/B).
-int splitk_counters(int slices, size_t slab_bytes, int64_t ntiles, bool list_ok, bool in_launch, unsigned **out) {
+int splitk_counters(int slices, size_t slab_bytes, int64_t ntiles, bool list_ok, bool in_launch, hipStream_t st,
+                    unsigned **out) {
   static const bool unfused = getenv("LK_SKP_UNFUSED") != nullptr, fused = getenv("LK_SKP_FUSED") != nullptr;
   *out = nullptr;
   if (!fused && (unfused || !in_launch)) return LK_OK;
   if (slices <= 1 || !list_ok || slab_bytes >= (1ull << 31) || ntiles <= 0) return LK_OK;
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   if (S.tcnt_n < (size_t)ntiles * kChainLine) {  // a 128-B line per tile
     const size_t want = std::max<size_t>((size_t)ntiles * kChainLine, 1 << 16);
-    if (S.tcnt) HIP_TRY(hipFree(S.tcnt));
-    S.tcnt = nullptr;
-    S.tcnt_n = 0;
-    HIP_TRY(hipMalloc((void **)&S.tcnt, want * sizeof(unsigned)));
-    HIP_TRY(hipMemset(S.tcnt, 0, want * sizeof(unsigned)));
-    S.tcnt_n = want;
+    void *p = S.tcnt;
+    size_t have = S.tcnt_n * sizeof(unsigned);
+    if (int rc = grow_scratch(S, &p, &have, want * sizeof(unsigned), true, st)) return rc;
+    S.tcnt = (unsigned *)p;
+    S.tcnt_n = have / sizeof(unsigned);
   }
   *out = S.tcnt;
+  return LK_OK;
+}
+
+// The per-tile counters of gemm_q_mfma_kernel / gemm_q_lds_kernel (zero between launches).
+int gemm_counters(size_t tiles, hipStream_t st, int32_t **out) {
+  GemmScratch &S = gemm_scratch(st);
+  if (S.counter_n < tiles) {
+    void *p = S.counter;
+    size_t have = S.counter_n * sizeof(int32_t);
+    if (int rc = grow_scratch(S, &p, &have, std::max<size_t>(tiles, 4096) * sizeof(int32_t), true, st)) return rc;
+    S.counter = (int32_t *)p;
+    S.counter_n = have / sizeof(int32_t);
+  }
+  *out = S.counter;
   return LK_OK;
 }
 
@@ -434,15 +511,7 @@ void launch_xsplit(const XSplitArgs &xa_in, hipStream_t st) {
   hipLaunchKernelGGL(xsplit_kernel, dim3((unsigned)(xa.xblocks + zblocks)), dim3(256), 0, st, xa);
 }
 
-int grow(void **p, size_t *have, size_t want) {
-  if (*have >= want) return LK_OK;
-  if (*p) HIP_TRY(hipFree(*p));
-  *p = nullptr;
-  *have = 0;
-  HIP_TRY(hipMalloc(p, want));
-  *have = want;
-  return LK_OK;
-}
+int grow(GemmScratch &S, void **p, size_t *have, size_t want) { return grow_scratch(S, p, have, want, false, nullptr); }
 
 int gemm_waves() {  // LK_GEMM_WAVES = 4 or 8 waves per LDS-GEMM workgroup (tuning only)
   static int nw = [] {
@@ -464,7 +533,7 @@ int gemm_occupancy() {  // LK_GEMM_OCC overrides (tuning only)
 template <int QT, int WM, int WN, int MT, int NT>
 int launch_gemm_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
   constexpr int BM = WM * MT * 16, BN = WN * NT * 16;
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   g.tiles_m = (g.M + BM - 1) / BM;
   g.tiles_n = (g.N + BN - 1) / BN;
   const int tiles = g.tiles_m * g.tiles_n;
@@ -475,20 +544,12 @@ int launch_gemm_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
   slices = (nblk + g.kslice - 1) / g.kslice;
   g.slices = slices;
   if (slices > 1) {
-    int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * tiles * BM * BN * sizeof(float));
+    int rc = grow(S, &S.partial, &S.partial_bytes, (size_t)slices * tiles * BM * BN * sizeof(float));
     if (rc) return rc;
-    if (S.counter_n < (size_t)tiles) {
-      void *c = S.counter;
-      size_t cb = S.counter_n * sizeof(int32_t);
-      rc = grow(&c, &cb, (size_t)tiles * sizeof(int32_t));
-      if (rc) return rc;
-      S.counter = (int32_t *)c;
-      S.counter_n = (size_t)tiles;
-      HIP_TRY(hipMemset(S.counter, 0, S.counter_n * sizeof(int32_t)));
-    }
+    if ((rc = gemm_counters((size_t)tiles, st, &g.counter))) return rc;
     g.partial = (float *)S.partial;
-    g.counter = S.counter;
   }
+  note_route("gemm_q_mfma<%d>:t%ds%d", QT, tiles, slices);
   launch_xsplit(xa, st);
   hipLaunchKernelGGL((gemm_q_mfma_kernel<QT, WM, WN, MT, NT>), dim3((unsigned)(tiles * slices)), dim3(256), 0, st, g);
   HIP_TRY(hipGetLastError());
@@ -511,7 +572,7 @@ bool gemm_lds_eligible(int32_t qt, const lk_tensor *a, const Checked &c) {
 template <int QT, int NT, int NW>
 int launch_gemm_lds_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
   using GG = LdsGemmGeom<QT, NT, NW>;
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   g.tiles_m = (g.M + GG::BM - 1) / GG::BM;
   g.tiles_n = (g.N + GG::BN - 1) / GG::BN;
   const int tiles = g.tiles_m * g.tiles_n;
@@ -521,20 +582,12 @@ int launch_gemm_lds_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
   slices = (g.K / 32 + g.kslice - 1) / g.kslice;
   g.slices = slices;
   if (slices > 1) {
-    int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * tiles * GG::BM * GG::BN * sizeof(float));
+    int rc = grow(S, &S.partial, &S.partial_bytes, (size_t)slices * tiles * GG::BM * GG::BN * sizeof(float));
     if (rc) return rc;
-    if (S.counter_n < (size_t)tiles) {
-      void *c = S.counter;
-      size_t cb = S.counter_n * sizeof(int32_t);
-      rc = grow(&c, &cb, (size_t)tiles * sizeof(int32_t));
-      if (rc) return rc;
-      S.counter = (int32_t *)c;
-      S.counter_n = (size_t)tiles;
-      HIP_TRY(hipMemset(S.counter, 0, S.counter_n * sizeof(int32_t)));
-    }
+    if ((rc = gemm_counters((size_t)tiles, st, &g.counter))) return rc;
     g.partial = (float *)S.partial;
-    g.counter = S.counter;
   }
+  note_route("gemm_q_lds<%d,%d,%d>:t%ds%d", QT, NT, NW, tiles, slices);
   launch_xsplit(xa, st);
   constexpr size_t lds = GG::LDS;
   hipLaunchKernelGGL((gemm_q_lds_kernel<QT, NT, NW>), dim3((unsigned)(tiles * slices)), dim3(NW * 64), lds, st, g);
@@ -569,7 +622,7 @@ bool skinny_eligible(const lk_tensor *a, const Checked &c) {
 template <int QT, int NT>
 int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
   using SG = SkinnyGeom<QT, NT>;
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   const int nblk = g.K / 32;
   const int slices = (nblk + SG::SB - 1) / SG::SB;
   const int ntile = (g.M + 15) / 16;
@@ -581,16 +634,17 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
   const bool list_ok = 1 + (g.tiles_per_range + SG::NW - 1) / SG::NW <= SG::D * SG::SLOT / 4;  // a wave's ring
-  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, false, &rsync)) return rf;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, false, st, &rsync)) return rf;
   g.slices = slices;
   if (slices > 1) {
-    const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
+    const int rc = grow(S, &S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
     if (rc) return rc;
     g.partial = (float *)S.partial;
   }
   g.tasks = ranges * slices;
   g.rsync = rsync;
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  note_route("skinny<%d,%d>:s%dr%d%s", QT, NT, slices, ranges, rsync ? "f" : "");
   hipLaunchKernelGGL((gemm_skinny_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
   if (slices > 1 && !rsync) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
@@ -605,7 +659,7 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
 template <int QT, int NT>
 int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   using SG = SkinnyPairGeom<QT, NT>;
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   const int nblk = g.K / 32;
   const int slices = (nblk + SG::SB - 1) / SG::SB;
   const int ntile = (g.M + 15) / 16;
@@ -617,17 +671,18 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
   const bool list_ok = 1 + (g.tiles_per_range + 3) / 4 <= NT * 64 * 4;  // parity 0 of a pair's hand-off
-  if (int rc = splitk_counters(slices, slab_bytes, ntile, list_ok, false, &rsync)) return rc;
+  if (int rc = splitk_counters(slices, slab_bytes, ntile, list_ok, false, st, &rsync)) return rc;
   const bool fuse = rsync != nullptr;
   g.slices = slices;
   if (slices > 1) {
-    const int rc = grow(&S.partial, &S.partial_bytes, slab_bytes);
+    const int rc = grow(S, &S.partial, &S.partial_bytes, slab_bytes);
     if (rc) return rc;
     g.partial = (float *)S.partial;
   }
   g.tasks = ranges * slices;
   g.rsync = rsync;
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  note_route("pair<%d,%d>:s%dr%d%s", QT, NT, slices, ranges, fuse ? "f" : "");
   hipLaunchKernelGGL((gemm_skinny_pair_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
   if (slices > 1 && !fuse) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
@@ -644,10 +699,10 @@ int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
 template <int QT, int NT>
 int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   using SG = SkGeom<QT, NT>;
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   const int64_t nblk = c.K / 32, ntx = (c.N + 15) / 16;
   const size_t fb = (size_t)ntx * nblk * kXSplits * 64 * 16, sb = (size_t)nblk * ntx * 16 * sizeof(float);
-  int rc = grow(&S.frag, &S.frag_bytes, fb + sb);
+  int rc = grow(S, &S.frag, &S.frag_bytes, fb + sb);
   if (rc) return rc;
   XSplitArgs xa{};
   xa.b = (const uint8_t *)b->data + b->data_offset;
@@ -672,10 +727,10 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
   const bool list_ok = 1 + (g.tiles_per_range + 3) / 4 <= NT * 64 * 4;  // parity 0 of a pair's hand-off
-  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, false, &rsync)) return rf;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * 16 * NT * sizeof(float), ntile, list_ok, false, st, &rsync)) return rf;
   g.slices = slices;
   if (slices > 1) {
-    rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
+    rc = grow(S, &S.partial, &S.partial_bytes, (size_t)slices * g.M * 16 * NT * sizeof(float));
     if (rc) return rc;
     g.partial = (float *)S.partial;
   }
@@ -685,6 +740,7 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
   g.fx = b->nb[0] == 4 && b->nb[1] == 4 * (uint64_t)c.N && ((uintptr_t)xa.b & 15) == 0;
   if (!g.fx) launch_xsplit(xa, st);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  note_route("sk<%d,%d>:s%dr%d%s", QT, NT, slices, ranges, rsync ? "f" : "");
   hipLaunchKernelGGL((gemm_sk_kernel<QT, NT>), dim3(grid), dim3(SG::NW * 64), SG::LDS, st, g);
   if (slices > 1 && !rsync) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
@@ -697,18 +753,29 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
 
 bool getenv_flag(const char *name);
 
+// True when p points into device memory of some HIP device (hipMalloc / torch tensors), false for
+// page-locked or pageable host memory.
+bool is_device_memory(const void *p) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeDevice;
+}
+
 // gemm_kpart_kernel (lk_kpart.hpp): Q4_0 / Q4_1 at 2 <= N <= 32, K split over the waves of a
 // workgroup (8·KB blocks per workgroup) and over slices of that span; per-tile sums in LDS, the
 // slices' slabs summed by the last arriver. One workgroup per CU (LDS); grids may exceed the CUs.
 template <int QT, int NT>
 int launch_kpart_t(const SkinnyArgs &s, hipStream_t st) {
   using KG = KpartGeom<QT, NT>;
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   // the activation fragments (xsplit_kernel) in the k order of QT's code decode, and T per (block,
   // column): Q4_0 −136·Σ(hi + lo) (codes 128 + n), Q4_1 Σx (codes n·2⁻⁹)
   const int64_t nblk = s.K / 32, ntx = (s.N + 15) / 16;
   const size_t fb = (size_t)ntx * nblk * kXSplits * 64 * 16, sb = (size_t)nblk * ntx * 16 * sizeof(float);
-  if (int rc = grow(&S.frag, &S.frag_bytes, fb + sb)) return rc;
+  if (int rc = grow(S, &S.frag, &S.frag_bytes, fb + sb)) return rc;
   XSplitArgs xa{};
   xa.b = s.b;
   xa.b_nb0 = s.b_nb0; xa.b_nb1 = s.b_nb1;
@@ -732,19 +799,22 @@ int launch_kpart_t(const SkinnyArgs &s, hipStream_t st) {
   // two K slices (C3's N = 32 at K = 4096): each adds its tile sums into dst, zeroed by the xsplit
   // launch — a + b is b + a, so the result does not depend on which slice adds first, and equals the
   // slab sum s0 + s1 (only −0.0 + −0.0 becomes +0.0). More slices: slabs and the last arriver.
+  // Only into device memory: float atomics on page-locked host memory (a resident graph's direct
+  // output regions, a caller's mapped buffer) go over PCIe, where their atomicity is not promised.
   static const bool no_atomic = getenv_flag("LK_KPART_NO_ATOMIC");
-  g.atomic_dst = slices == 2 && !no_atomic;
+  g.atomic_dst = slices == 2 && !no_atomic && is_device_memory(s.dst);
   if (g.atomic_dst) {
     xa.zero = s.dst; xa.z_nb0 = s.d_nb0; xa.z_nb1 = s.d_nb1; xa.zM = s.M; xa.zN = s.N;
   } else if (slices > 1) {
     const size_t slab_bytes = (size_t)slices * g.M * 16 * NT * sizeof(float);
-    if (int rc = grow(&S.partial, &S.partial_bytes, slab_bytes)) return rc;
+    if (int rc = grow(S, &S.partial, &S.partial_bytes, slab_bytes)) return rc;
     g.partial = (float *)S.partial;
-    if (int rc = splitk_counters(slices, slab_bytes, ntile, true, false, &g.tcnt)) return rc;
+    if (int rc = splitk_counters(slices, slab_bytes, ntile, true, false, st, &g.tcnt)) return rc;
   }
   g.tasks = ranges * slices;
   launch_xsplit(xa, st);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  note_route("kpart<%d,%d>:s%dr%d%s", QT, NT, slices, ranges, g.atomic_dst ? "a" : g.tcnt ? "f" : "");
   hipLaunchKernelGGL((gemm_kpart_kernel<QT, NT>), dim3(grid), dim3(KG::NW * 64), KG::LDS, st, g);
   if (slices > 1 && !g.tcnt && !g.atomic_dst) {
     const int64_t threads = (int64_t)g.M * (16 * NT / 4);
@@ -802,7 +872,7 @@ int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
     xa.mult = -136.f;
   }
   using WG = WideGeom<QT>;
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   g.tiles_m = (g.M + WG::BM - 1) / WG::BM;
   g.tiles_n = (g.N + WG::BN - 1) / WG::BN;
   const int tiles = g.tiles_m * g.tiles_n;
@@ -813,7 +883,7 @@ int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
   g.slices = slices;
   const int npad = g.tiles_n * WG::BN;
   if (slices > 1) {
-    const int rc = grow(&S.partial, &S.partial_bytes, (size_t)slices * g.M * npad * sizeof(float));
+    const int rc = grow(S, &S.partial, &S.partial_bytes, (size_t)slices * g.M * npad * sizeof(float));
     if (rc) return rc;
     g.partial = (float *)S.partial;
   }
@@ -833,9 +903,10 @@ int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
   g.tasks = nsuper * g.sm * g.sn * slices;
   // split-K fixed up inside gemm_wide_kernel by the last arriver per tile (splitk_counters)
   g.rsync = nullptr;
-  if (int rf = splitk_counters(slices, (size_t)slices * g.M * npad * sizeof(float), tiles, true, true, &g.rsync)) return rf;
+  if (int rf = splitk_counters(slices, (size_t)slices * g.M * npad * sizeof(float), tiles, true, true, st, &g.rsync)) return rf;
   launch_xsplit(xa, st);
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  note_route("wide<%d>:t%ds%d%s", QT, tiles, slices, g.rsync ? "f" : "");
   hipLaunchKernelGGL((gemm_wide_kernel<QT>), dim3(grid), dim3(WG::NW * 64), WG::LDS, st, g);
   if (slices > 1 && !g.rsync) {
     const int64_t threads = (int64_t)g.M * (npad / 4);
@@ -847,10 +918,10 @@ int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
 }
 
 int launch_gemm(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
-  GemmScratch &S = gemm_scratch();
+  GemmScratch &S = gemm_scratch(st);
   const int64_t nblk = c.K / 32, ntx = (c.N + 15) / 16;
   const size_t fb = (size_t)ntx * nblk * kXSplits * 64 * 16, sb = (size_t)nblk * ntx * 16 * sizeof(float);
-  int rc = grow(&S.frag, &S.frag_bytes, fb + sb);
+  int rc = grow(S, &S.frag, &S.frag_bytes, fb + sb);
   if (rc) return rc;
   XSplitArgs xa{};
   xa.b = (const uint8_t *)b->data + b->data_offset;
@@ -922,6 +993,7 @@ int launch_f32_mfma(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, cons
   const bool dense = v4 && g.b_nb0 == 4 && g.b_nb1 % 16 == 0 && ((uintptr_t)g.b & 15) == 0 && c.K % kF32Chunk == 0 &&
                      c.N % 4 == 0 && (c.M - 1) * g.a_nb1 + 4 * c.K < (1ll << 32) && c.K * g.b_nb1 < (1ll << 32) &&
                      !f32_direct;
+  note_route(dense ? "f32_lds" : v4 ? "f32_mfma<1>" : "f32_mfma<0>");
   if (dense) hipLaunchKernelGGL(f32_lds_kernel, grid, block, 4 * 32768, st, g);
   else if (v4) hipLaunchKernelGGL(f32_mfma_kernel<true>, grid, block, 0, st, g);
   else hipLaunchKernelGGL(f32_mfma_kernel<false>, grid, block, 0, st, g);
@@ -936,6 +1008,7 @@ int launch_generic(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const
   if (blocks > (int64_t)INT32_MAX) return fail(LK_ERR_NOT_IMPLEMENTED, "output too large for the generic kernel");
   dim3 grid((unsigned)blocks), block(256);
   int32_t t = (c.path == Path::kQuantF32) ? a->type : (c.path == Path::kF32 ? LK_TYPE_F32 : LK_TYPE_F16);
+  note_route("generic<%d>", t);
   switch (t) {
     case LK_TYPE_Q4_0: hipLaunchKernelGGL(mul_mat_generic_kernel<LK_TYPE_Q4_0>, grid, block, 0, st, g); break;
     case LK_TYPE_Q4_1: hipLaunchKernelGGL(mul_mat_generic_kernel<LK_TYPE_Q4_1>, grid, block, 0, st, g); break;
@@ -975,6 +1048,7 @@ void launch_kq_nc(int nc, dim3 grid, dim3 block, size_t lds, hipStream_t st, con
 // otherwise (the Kotlin full-block quirk / flat partial path) kquant_mul_mat_kernel, one wave
 // per output. LK_KQ_LEGACY (set) forces the latter (lab A/B).
 int launch_kquant(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  note_route("kquant<%d>", a->type);
   KQuantArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
   g.b = (const uint8_t *)b->data + b->data_offset;
@@ -1174,7 +1248,7 @@ int pin_on(int d, const lk_tensor *a, uint64_t lo, uint64_t bytes, uint64_t gene
   drop_overlapping(v, base, lo, lo + bytes, true, generation);
   auto m = std::make_shared<Mirror>();
   m->dev = d; m->base = base; m->lo = lo; m->bytes = bytes; m->gen = generation;
-  HIP_TRY(hipMalloc(&m->ptr, std::max<uint64_t>(bytes, 4)));
+  HIP_TRY(hipMalloc(&m->ptr, bytes + kASlack));
   HIP_TRY(hipMemcpy(m->ptr, (const uint8_t *)a->data + lo, bytes, hipMemcpyHostToDevice));
   v.weights.push_back(m);
   v.weight_bytes += bytes;
@@ -1207,6 +1281,20 @@ extern "C" {
 const char *lk_version(void) { return "lk_hip 0.1 (gfx950)"; }
 
 const char *lk_last_error(void) { return g_err.c_str(); }
+
+const char *lk_debug_route(void) { return g_route.c_str(); }
+
+void lk_debug_route_clear(void) { g_route.clear(); }
+
+uint64_t lk_debug_scratch_epoch(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  uint64_t e = 0;
+  for (auto &kv : scratch_map())
+    if (kv.first.dev == dev) e += kv.second.epoch;
+  return e;
+}
 
 int lk_device_count(void) {
   int n = 0;
@@ -1284,6 +1372,18 @@ void lk_shutdown(void) {
     (void)hipStreamDestroy(v.stream);
     v.stream = nullptr;
   }
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto &kv : scratch_map()) {
+      (void)hipSetDevice(kv.first.dev);
+      (void)hipDeviceSynchronize();
+      GemmScratch &G = kv.second;
+      for (void *p : G.retired) (void)hipFree(p);
+      for (void *p : {G.frag, G.partial, (void *)G.counter, (void *)G.tcnt})
+        if (p) (void)hipFree(p);
+    }
+    scratch_map().clear();
+  }
   lk_weights_evict_all();
   (void)hipSetDevice(prev);
   s.device = -1;
@@ -1327,8 +1427,11 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   // A: cached mirror or staged copy
   const MirrorRef pinned = find_pinned(s, a->data, c.a_lo, c.a_hi);  // held for the call
   const void *a_dev = pinned ? (const uint8_t *)pinned->ptr + (c.a_lo - pinned->lo) : nullptr;
+  if (pinned) note_route("A=mirror[%llu,+%llu)g%llu", (unsigned long long)pinned->lo, (unsigned long long)pinned->bytes,
+                         (unsigned long long)pinned->gen);
+  else note_route("A=staged");
   if (!a_dev && a_bytes) {
-    if ((rc = ensure_scratch(s, 0, a_bytes))) return rc;
+    if ((rc = ensure_scratch(s, 0, a_bytes + kASlack))) return rc;
     HIP_TRY(hipMemcpyAsync(s.scratch[0], (const uint8_t *)a->data + c.a_lo, a_bytes, hipMemcpyHostToDevice, st));
     a_dev = s.scratch[0];
   }
@@ -1338,7 +1441,9 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   // strided dst: preserve the bytes between written elements
   HIP_TRY(hipMemcpyAsync(s.scratch[2], (const uint8_t *)dst->data + c.d_lo, d_bytes, hipMemcpyHostToDevice, st));
   lk_tensor da = *a, db = *b, dd = *dst;
-  da.data = const_cast<void *>(a_dev); da.data_offset = 0; da.buf_bytes = a_bytes;
+  // A's device copy (mirror or staging) has kASlack readable bytes past the matrix
+  da.data = const_cast<void *>(a_dev); da.data_offset = 0;
+  da.buf_bytes = pinned ? pinned->lo + pinned->bytes + kASlack - c.a_lo : a_bytes + kASlack;
   db.data = s.scratch[1]; db.data_offset = 0; db.buf_bytes = b_bytes;
   dd.data = s.scratch[2]; dd.data_offset = 0; dd.buf_bytes = d_bytes;
   Checked cd = c;
@@ -1385,6 +1490,10 @@ struct Shard {
 }  // namespace
 
 int lk_weights_pin_sharded(const lk_tensor *a, uint64_t generation, int n_shards) {
+  return lk_weights_pin_sharded_at(a, generation, n_shards, 0);
+}
+
+int lk_weights_pin_sharded_at(const lk_tensor *a, uint64_t generation, int n_shards, int first_device) {
   if (!a || !a->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(LK_ERR_DEVICE, "no HIP device visible");
@@ -1400,7 +1509,7 @@ int lk_weights_pin_sharded(const lk_tensor *a, uint64_t generation, int n_shards
     int64_t r0, r1;
     shard_span(a->ne[1], n_shards, r, &r0, &r1);
     if (r1 <= r0) continue;
-    const int d = r % std::min(ndev, kMaxDevices);
+    const int d = (first_device + r) % std::min(ndev, kMaxDevices);
     if ((rc = init_dev(d))) break;
     rc = pin_on(d, a, a->data_offset + (uint64_t)r0 * pitch, (uint64_t)(r1 - r0) * pitch, generation);
   }
@@ -1409,10 +1518,15 @@ int lk_weights_pin_sharded(const lk_tensor *a, uint64_t generation, int n_shards
 }
 
 int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, int n_shards) {
+  return lk_mul_mat_sharded_at(a, b, dst, n_shards, 0);
+}
+
+int lk_mul_mat_sharded_at(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, int n_shards, int first_device) {
   Checked c;
   int rc = check(a, b, dst, &c);
   if (rc) return rc;
   if (n_shards < 1) return fail(LK_ERR_INVALID_ARG, "n_shards %d", n_shards);
+  if (first_device < 0) return fail(LK_ERR_INVALID_ARG, "first_device %d", first_device);
   if (c.empty) return LK_OK;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(LK_ERR_DEVICE, "no HIP device visible");
@@ -1423,7 +1537,17 @@ int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, i
   const uint64_t ew = dst->type == LK_TYPE_F16 ? 2 : 4;
   const bool rows_ok = pitch && (uint64_t)(c.N - 1) * dst->nb[0] + ew <= dst->nb[1];
   const int P = rows_ok ? (int)std::min<int64_t>(n_shards, c.M) : 1;
-  if (P == 1) return lk_mul_mat(a, b, dst);
+  if (P == 1) {  // one device: first_device's
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    int rc1 = init_dev(first_device % ndev);
+    if (rc1 == LK_OK) {
+      S().device = first_device % ndev;
+      rc1 = lk_mul_mat(a, b, dst);
+    }
+    (void)hipSetDevice(prev);
+    return rc1;
+  }
 
   int prev = 0;
   (void)hipGetDevice(&prev);
@@ -1433,7 +1557,7 @@ int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, i
     shard_span(c.M, P, r, &r0, &r1);
     if (r1 <= r0) continue;
     Shard x{};
-    x.dev = r % ndev;
+    x.dev = (first_device + r) % ndev;
     x.a = *a; x.a.ne[1] = r1 - r0; x.a.data_offset = a->data_offset + (uint64_t)r0 * pitch;
     x.d = *dst; x.d.ne[1] = r1 - r0; x.d.data_offset = dst->data_offset + (uint64_t)r0 * dst->nb[1];
     if ((rc = check(&x.a, b, &x.d, &x.c))) return rc;
@@ -1452,7 +1576,7 @@ int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, i
     x.pin = find_pinned(v, a->data, x.c.a_lo, x.c.a_hi);
     x.a_dev = x.pin ? (const uint8_t *)x.pin->ptr + (x.c.a_lo - x.pin->lo) : nullptr;
     x.a_stage_off = a_need[x.dev];
-    if (!x.a_dev) a_need[x.dev] += (x.c.a_hi - x.c.a_lo + 255) & ~255ull;
+    if (!x.a_dev) a_need[x.dev] += (x.c.a_hi - x.c.a_lo + kASlack + 255) & ~255ull;
     x.d_off = d_need[x.dev];
     d_need[x.dev] += (x.c.d_hi - x.c.d_lo + 255) & ~255ull;
   }
@@ -1480,7 +1604,8 @@ int lk_mul_mat_sharded(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, i
     if (hipMemcpyAsync(d_dev, (const uint8_t *)dst->data + x.c.d_lo, db, hipMemcpyHostToDevice, v.stream) !=
         hipSuccess) { rc = fail(LK_ERR_DEVICE, "sharded: dst upload"); goto out; }
     lk_tensor da = x.a, dbt = *b, dd = x.d;
-    da.data = const_cast<void *>(a_dev); da.data_offset = 0; da.buf_bytes = ab;
+    da.data = const_cast<void *>(a_dev); da.data_offset = 0;
+    da.buf_bytes = x.pin ? x.pin->lo + x.pin->bytes + kASlack - x.c.a_lo : ab + kASlack;
     dbt.data = v.scratch[1]; dbt.data_offset = 0; dbt.buf_bytes = b_bytes;
     dd.data = d_dev; dd.data_offset = 0; dd.buf_bytes = db;
     Checked cd = x.c;
@@ -1794,12 +1919,24 @@ int lk_sync_counters_sum(uint64_t *sum) {
   int rc = ensure_init();
   if (rc) return rc;
   *sum = 0;
-  GemmScratch &G = gemm_scratch();
-  if (!G.tcnt) return LK_OK;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   HIP_TRY(hipDeviceSynchronize());
-  std::vector<unsigned> w(G.tcnt_n);
-  HIP_TRY(hipMemcpy(w.data(), G.tcnt, w.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
-  for (unsigned x : w) *sum += x;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  for (auto &kv : scratch_map()) {  // every stream's scratch on this device
+    if (kv.first.dev != dev) continue;
+    const GemmScratch &G = kv.second;
+    if (G.tcnt) {
+      std::vector<unsigned> w(G.tcnt_n);
+      HIP_TRY(hipMemcpy(w.data(), G.tcnt, w.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+      for (unsigned x : w) *sum += x;
+    }
+    if (G.counter) {  // gemm_q_mfma_kernel / gemm_q_lds_kernel tile counters
+      std::vector<int32_t> w(G.counter_n);
+      HIP_TRY(hipMemcpy(w.data(), G.counter, w.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+      for (int32_t x : w) *sum += (uint32_t)x;
+    }
+  }
   return LK_OK;
 }
 
@@ -2027,7 +2164,7 @@ int graph_bind(lk_graph *g, bool at_create) {
     lk_tensor &d = g->shard[i] ? g->sa[i] : g->da[i];
     d = src;
     d.data = (uint8_t *)m->ptr + (lo - m->lo) - lo;  // base shifted: base + offset = mirror
-    d.buf_bytes = hi;
+    d.buf_bytes = m->lo + m->bytes + kASlack;          // the mirror's end, its slack included
   }
   for (int l = 0; l < g->nlev; l++) {
     std::vector<lk_tensor> la, lb, ld, sa, sb, sd;

@@ -96,6 +96,7 @@ struct lk_p2p_group {
   std::vector<lk_p2p_plan *> tail;
   std::vector<uint64_t> tail_target;
   uint64_t plans_alive = 0;
+  bool destroyed = false;  // lk_p2p_group_destroy ran while plans were alive: the last plan deletes the group
   bool broken = false;  // a launch failed after some ranks enqueued theirs: later gates could never open
 };
 
@@ -137,9 +138,11 @@ int lk_p2p_group_create(int nranks, const int *devices, lk_p2p_group **out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return lk_detail_fail(LK_ERR_DEVICE, "p2p group: no device");
   for (int r = 0; r < nranks; r++)
     if (devices[r] < 0 || devices[r] >= ndev) return lk_detail_fail(LK_ERR_INVALID_ARG, "p2p group: no such device");
-  int ok = 1;
-  if (hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, devices[0]) != hipSuccess || !ok)
-    return lk_detail_fail(LK_ERR_DEVICE, "p2p group: device cannot gate a stream on a memory value");
+  for (int r = 0; r < nranks; r++) {  // every rank's stream is gated on a memory value
+    int ok = 1;
+    if (hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, devices[r]) != hipSuccess || !ok)
+      return lk_detail_fail(LK_ERR_DEVICE, "p2p group: a device cannot gate a stream on a memory value");
+  }
   for (int r = 0; r < nranks; r++) {
     int rc = lk_init(devices[r]);
     if (rc) return rc;
@@ -172,7 +175,16 @@ int lk_p2p_group_create(int nranks, const int *devices, lk_p2p_group **out) {
 
 int lk_p2p_group_nranks(const lk_p2p_group *g) { return g ? g->P : 0; }
 
-void lk_p2p_group_destroy(lk_p2p_group *g) { delete g; }
+// A group with live plans is only marked: each plan holds a pointer to it, and the last plan's
+// destroy deletes it (a caller closing the group before its plans must not leave them dangling).
+void lk_p2p_group_destroy(lk_p2p_group *g) {
+  if (!g) return;
+  if (g->plans_alive) {
+    g->destroyed = true;
+    return;
+  }
+  delete g;
+}
 
 int lk_p2p_plan_create(lk_p2p_group *g, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
                        lk_p2p_plan **out) {
@@ -327,6 +339,7 @@ void lk_p2p_plan_destroy(lk_p2p_plan *p) {
     if (g->tail[r] == p) g->tail[r] = nullptr;  // the caller synchronized: nothing left to gate on
   g->plans_alive--;
   free_plan(p);
+  if (g->destroyed && g->plans_alive == 0) delete g;
 }
 
 }  // extern "C"

@@ -74,8 +74,10 @@ def raise_for_status(status: int, msg: str):
 EXPORTED_SYMBOLS = (
     "lk_init", "lk_device_count", "lk_last_error", "lk_shutdown", "lk_version",
     "lk_mul_mat_validate", "lk_mul_mat", "lk_mul_mat_device", "lk_mul_mat_sharded", "lk_weights_pin_sharded",
+    "lk_mul_mat_sharded_at", "lk_weights_pin_sharded_at",
     "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy", "lk_plan_create_chain",
     "lk_plan_chain_timed_out", "lk_sync_timeouts", "lk_set_sync_wait_bound", "lk_sync_counters_sum",
+    "lk_debug_route", "lk_debug_route_clear", "lk_debug_scratch_epoch",
     "lk_graph_create", "lk_graph_create_sharded", "lk_graph_num_sharded", "lk_graph_compute",
     "lk_graph_num_levels", "lk_graph_num_launches",
     "lk_graph_transfer_bytes", "lk_graph_destroy", "lk_graph_num_rebinds",
@@ -125,6 +127,9 @@ def load():
     L.lk_mul_mat_device.argtypes = [P, P, P, vp]
     L.lk_mul_mat_sharded.argtypes = [P, P, P, ctypes.c_int]
     L.lk_weights_pin_sharded.argtypes = [P, ctypes.c_uint64, ctypes.c_int]
+    if hasattr(L, "lk_mul_mat_sharded_at"):  # (absent from round-4 lab builds loaded for A/B)
+        L.lk_mul_mat_sharded_at.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int]
+        L.lk_weights_pin_sharded_at.argtypes = [P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
     L.lk_plan_create.argtypes = [P, P, P, ctypes.c_int, ctypes.POINTER(vp)]
     L.lk_plan_launch.argtypes = [vp, vp]
     L.lk_plan_create_chain.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.POINTER(vp)]
@@ -132,6 +137,10 @@ def load():
     L.lk_sync_timeouts.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
     L.lk_set_sync_wait_bound.argtypes = [ctypes.c_uint64]
     L.lk_sync_counters_sum.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(L, "lk_debug_route"):  # (absent from round-4 lab builds loaded for A/B)
+        L.lk_debug_route.restype = ctypes.c_char_p
+        L.lk_debug_route_clear.restype = None
+        L.lk_debug_scratch_epoch.restype = ctypes.c_uint64
     L.lk_plan_num_launches.argtypes = [vp]
     L.lk_plan_destroy.argtypes = [vp]
     L.lk_plan_destroy.restype = None

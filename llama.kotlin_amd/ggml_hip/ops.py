@@ -102,14 +102,15 @@ def computeMatMul(graphAllocator: GGMLGraphAllocator, context: GGMLContext | Non
 
 
 def computeMatMulSharded(graphAllocator: GGMLGraphAllocator, context: GGMLContext | None, a: GGMLTensor,
-                         b: GGMLTensor, dst: GGMLTensor, nShards: int) -> None:
+                         b: GGMLTensor, dst: GGMLTensor, nShards: int, firstDevice: int = 0) -> None:
     """computeMatMul over host buffers with A's rows split over nShards GPUs of this process
-    (lk_mul_mat_sharded; shard r on device r mod device count). Same results as computeMatMul."""
+    (lk_mul_mat_sharded_at; shard r on device (firstDevice + r) mod device count). Same results as
+    computeMatMul."""
     if not all(_is_host(graphAllocator, t) for t in (a, b, dst)):
         raise _lib.IllegalArgumentException("computeMatMulSharded takes host (ByteArray) buffers")
     L = _lib.load()
     la, lb, ld = to_lk(graphAllocator, a), to_lk(graphAllocator, b), to_lk(graphAllocator, dst)
-    _lib.check(L.lk_mul_mat_sharded(ctypes.byref(la), ctypes.byref(lb), ctypes.byref(ld), int(nShards)))
+    _lib.check(L.lk_mul_mat_sharded_at(ctypes.byref(la), ctypes.byref(lb), ctypes.byref(ld), int(nShards), int(firstDevice)))
 
 
 def validateMatMul(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, b: GGMLTensor, dst: GGMLTensor) -> int:
@@ -346,9 +347,11 @@ def weightsCachedCount() -> int:
     return int(_lib.load().lk_weights_cached_count())
 
 
-def weightsPinSharded(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, nShards: int, generation: int = 0):
+def weightsPinSharded(graphAllocator: GGMLGraphAllocator, a: GGMLTensor, nShards: int, generation: int = 0,
+                      firstDevice: int = 0):
     """Pin each row shard of a on the device computeMatMulSharded runs it on."""
-    _lib.check(_lib.load().lk_weights_pin_sharded(ctypes.byref(to_lk(graphAllocator, a)), generation, int(nShards)))
+    _lib.check(_lib.load().lk_weights_pin_sharded_at(ctypes.byref(to_lk(graphAllocator, a)), generation, int(nShards),
+                                                     int(firstDevice)))
 
 
 def syncTimeouts() -> int:
@@ -376,5 +379,22 @@ def weightsEvictAll():
     _lib.load().lk_weights_evict_all()
 
 
-__all__ = ["syncTimeouts", "setSyncWaitBound", "syncCountersSum", "computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+def debugRoute(clear: bool = True) -> str:
+    """The kernels this thread's calls launched since the last clear (lk_debug_route), e.g.
+    "A=mirror[0,+55296)g0 gemm_q_mfma<2>:t2s12"; '' from a library built without it."""
+    L = _lib.load()
+    if not hasattr(L, "lk_debug_route"):
+        return ""
+    r = L.lk_debug_route().decode(errors="replace")
+    if clear:
+        L.lk_debug_route_clear()
+    return r
+
+
+def debugScratchEpoch() -> int:
+    """Reallocations of the current device's batched-kernel scratch so far (lk_debug_scratch_epoch)."""
+    return int(_lib.load().lk_debug_scratch_epoch())
+
+
+__all__ = ["syncTimeouts", "setSyncWaitBound", "syncCountersSum", "debugRoute", "debugScratchEpoch", "computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
            "weightsEvictAll", "weightsEvict", "weightsEvictBuffer", "weightsCachedBytes", "weightsCachedCount", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]

@@ -164,6 +164,12 @@ class Comm:
         return _lib.load().lk_comm_device(self._handle)
 
     @property
+    def rcclRanks(self) -> int:
+        """The rank count the C-ABI communicator holds (lk_comm_nranks: what RCCL was initialised with)."""
+        from . import _lib
+        return int(_lib.load().lk_comm_nranks(self._handle))
+
+    @property
     def numCollectives(self) -> int:
         """ncclAllGather calls enqueued through this communicator so far."""
         from . import _lib

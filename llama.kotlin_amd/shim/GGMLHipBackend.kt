@@ -56,7 +56,7 @@ private fun fill(t: lk_tensor, src: GGMLTensor, base: CPointer<ByteVar>?, bytes:
  */
 fun computeMatMulHip(graphAllocator: GGMLGraphAllocator, @Suppress("unused") context: GGMLContext,
                      a: GGMLTensor, b: GGMLTensor, dst: GGMLTensor, weightGeneration: ULong = 0u,
-                     shards: Int = 1) {
+                     shards: Int = 1, firstDevice: Int = 0) {
     val bufA = graphAllocator.buffers.getOrNull(a.bufferId)
     val bufB = graphAllocator.buffers.getOrNull(b.bufferId)
     val bufD = graphAllocator.buffers.getOrNull(dst.bufferId)
@@ -73,9 +73,10 @@ fun computeMatMulHip(graphAllocator: GGMLGraphAllocator, @Suppress("unused") con
                     fill(ld, dst, if (bufD != null && bufD.isNotEmpty()) pd.addressOf(0) else null, bufD?.size ?: 0)
                     val quant = a.type == GGMLType.Q4_0 || a.type == GGMLType.Q4_1 || a.type == GGMLType.Q8_0
                     if (shards > 1) {
-                        // rows of A over the node's GPUs (shard r on device r mod lk_device_count())
-                        if (quant && a.ne[0] % 32L == 0L) checkStatus(lk_weights_pin_sharded(la.ptr, weightGeneration, shards))
-                        checkStatus(lk_mul_mat_sharded(la.ptr, lb.ptr, ld.ptr, shards))
+                        // rows of A over the node's GPUs (shard r on device (firstDevice + r) mod lk_device_count())
+                        if (quant && a.ne[0] % 32L == 0L)
+                            checkStatus(lk_weights_pin_sharded_at(la.ptr, weightGeneration, shards, firstDevice))
+                        checkStatus(lk_mul_mat_sharded_at(la.ptr, lb.ptr, ld.ptr, shards, firstDevice))
                     } else {
                         if (quant) checkStatus(lk_weights_pin(la.ptr, weightGeneration))
                         checkStatus(lk_mul_mat(la.ptr, lb.ptr, ld.ptr))
@@ -260,7 +261,7 @@ class GGMLHipBackend(private val device: Int = 0, private val shards: Int = 1,
                     // row shards node by node through the host dst (lk_mul_mat_sharded)
                     for (k in i until j) {
                         val n = nodes[k]
-                        computeMatMulHip(ga, GGMLContext(), n.src[0]!!, n.src[1]!!, n, weightGeneration, shards)
+                        computeMatMulHip(ga, GGMLContext(), n.src[0]!!, n.src[1]!!, n, weightGeneration, shards, device)
                     }
                 } else {
                     computeRun(ga, nodes, i, j)  // one lk_graph (row-sharded over the GPUs with comms)

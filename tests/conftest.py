@@ -23,6 +23,26 @@ def oracle():
     return O
 
 
+@pytest.fixture(autouse=True)
+def _counter_trace(request):
+    """Lab diagnostic (LK_DIAG_COUNTERS=<file>): the split-K counter sum after every GPU test, so the
+    first test that leaves a counter armed is named. Off by default."""
+    path = os.environ.get("LK_DIAG_COUNTERS")
+    yield
+    if not path or request.node.get_closest_marker("gpu") is None:
+        return
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return
+        import ggml_hip as G
+        v = G.syncCountersSum()
+    except Exception as e:  # noqa: BLE001 — diagnostic only
+        v = f"error {e}"
+    with open(path, "a") as f:
+        f.write(f"{request.node.nodeid} {v}\n")
+
+
 @pytest.fixture(scope="session")
 def gpu():
     """Device + the HIP backend library; fails (not skips) when the library is missing."""

@@ -2,6 +2,8 @@
 ByteArray-backed tensors computed with the activations kept in HBM between nodes. Every
 result must equal the same nodes run one computeMatMul at a time (bit for bit: the same
 kernels compute each node), and only graph inputs may cross PCIe on the way in."""
+import os
+
 import numpy as np
 import pytest
 
@@ -38,32 +40,81 @@ def _layer(ga, oracle, K=256, F=384, N=1, seed=0):
     return x, nodes
 
 
-def _sequential(ga, nodes):
+def _sequential(ga, nodes, routes=None):
     import ggml_hip as G
     for a, b, d in nodes:
+        G.debugRoute()
         G.computeMatMul(ga, ga.context, a, b, d)
+        if routes is not None:
+            routes.append(G.debugRoute())
     return [bytes(ga.tensorBytes(d)) for _, _, d in nodes]
+
+
+NAMES = ["q", "k", "v", "o", "g", "u", "d"]
+
+
+def _oracle_check(ga, oracle, nodes, x, got):
+    """Each node's bytes against the oracle on the inputs the node read (x, or the producing node's
+    result in `got`: o reads q, d reads u). Returns {name: (ok, msg)}."""
+    from test_gpu_parity import noise_for
+    from _util import parity_ok
+    out = {}
+    xin = np.frombuffer(bytes(ga.tensorBytes(x)), np.float32)
+    for i, (a, b, d) in enumerate(nodes):
+        N, K, M = b.ne[0], a.ne[0], a.ne[1]
+        src = {3: 0, 6: 5}.get(i)
+        bv = xin if src is None else np.frombuffer(got[src], np.float32)
+        xk = bv.reshape(K, N)
+        q = np.frombuffer(bytes(ga.tensorBytes(a)), np.uint8)
+        ref = oracle.mat_mul_q(int(a.type), q, M, K, xk)
+        g = np.frombuffer(got[i], np.float32).reshape(M, N)
+        out[NAMES[i]] = parity_ok(g, ref, noise=noise_for(oracle, int(a.type), q, M, K, xk))
+    return out
 
 
 @pytest.mark.parametrize("N", [1, 4])
 def test_layer_graph_equals_sequential(gpu, oracle, N):
+    """The resident graph and the node-by-node path must agree bit for bit, and BOTH must meet the
+    parity bar against the oracle: a difference says which side is wrong, and the failure message
+    carries the kernel route of every node (lk_debug_route) and the split-K counter state."""
     import ggml_hip as G
+    assert G.syncCountersSum() == 0, "split-K counters not re-armed before the test"
     ga = G.GGMLGraphAllocator(device="host", defaultBufferSize=1 << 20)
     x, nodes = _layer(ga, oracle, N=N)
-    want = _sequential(ga, nodes)
+    routes = []
+    want = _sequential(ga, nodes, routes)
+    seq_ok = _oracle_check(ga, oracle, nodes, x, want)
     for _, _, d in nodes:
         ga.setTensorBytes(d, np.zeros(4 * d.ne[0] * d.ne[1], np.uint8))
     g = G.ResidentGraph(ga, nodes)
     assert g.numLevels == 2
     assert g.transferBytes(True) == 4 * N * 256  # only x goes up: weights pinned, q and u stay in HBM
     assert g.transferBytes(False) == sum(4 * d.ne[0] * d.ne[1] for _, _, d in nodes)
+    G.debugRoute()
     g.compute()
-    assert [bytes(ga.tensorBytes(d)) for _, _, d in nodes] == want
-    # a new input is picked up by the next compute
+    groute = G.debugRoute()
+    got = [bytes(ga.tensorBytes(d)) for _, _, d in nodes]
+    graph_ok = _oracle_check(ga, oracle, nodes, x, got)
+    ctr = G.syncCountersSum()
+    diag = "\n".join(f"  {n}: node-by-node {seq_ok[n]} route [{r}] | graph {graph_ok[n]}"
+                      for n, r in zip(NAMES, routes)) + f"\n  graph route [{groute}]\n  counters {ctr}"
+    if os.environ.get("LK_DIAG_DUMP") and not all(ok for ok, _ in seq_ok.values()):  # lab diagnostic
+        np.savez(os.environ["LK_DIAG_DUMP"], want=np.frombuffer(want[6], np.float32), got=np.frombuffer(got[6], np.float32),
+                 u=np.frombuffer(want[5], np.float32), wd=np.frombuffer(bytes(ga.tensorBytes(nodes[6][0])), np.uint8))
+    assert all(ok for ok, _ in seq_ok.values()), "node-by-node result off the oracle:\n" + diag
+    assert all(ok for ok, _ in graph_ok.values()), "graph result off the oracle:\n" + diag
+    assert got == want, "graph != node-by-node (both within the bar):\n" + diag
+    assert ctr == 0, diag
+    # a new input is picked up by the next compute (the captured replay from here on)
     ga.setTensorBytes(x, random_acts(256 * N, 99))
     want2 = _sequential(ga, nodes)
     g.compute()
+    got2 = [bytes(ga.tensorBytes(d)) for _, _, d in nodes]
+    assert all(ok for ok, _ in _oracle_check(ga, oracle, nodes, x, got2).values())
+    assert got2 == want2
+    g.compute()  # replayed again: the same bytes
     assert [bytes(ga.tensorBytes(d)) for _, _, d in nodes] == want2
+    assert G.syncCountersSum() == 0
 
 
 def test_outputs_mask_keeps_intermediates_on_device(gpu, oracle):
