@@ -305,6 +305,28 @@ int lk_p2p_plan_launch(lk_p2p_plan *plan, void *const *streams);
 uint64_t lk_p2p_plan_num_launches(const lk_p2p_plan *plan);
 int lk_p2p_plan_signal(lk_p2p_plan *plan, int rank, uint64_t *value);
 void lk_p2p_plan_destroy(lk_p2p_plan *plan);
+/* The persistent form of the same partition: a CHAIN of dependent stages of N = 1 nodes
+ * (lk_plan_create_chain's semantics: node i in stage stage[i]) as ONE launch per rank. Rank r's
+ * launch streams its row shard of every node; each row it computes is stored into its own full dst
+ * and into every other rank's (system-scope stores: xGMI on a node); the grid barrier between stages
+ * waits until EVERY rank has completed the stage (the rank that completes its stage adds 1 to a
+ * monotonic arrival word of every rank), so stage s + 1 reads whole activations. No host gate, no
+ * collective, no extra launch per layer. Tensors rank-major as lk_p2p_plan_create, every dst a dense
+ * F32 [1, M] (N = 1 streaming nodes of one quant type), and every rank's dst tensors laid out alike
+ * (one byte offset per pair of ranks over all nodes). Ranks on one device share its CUs and need
+ * streams of their own (they wait for each other inside their launches). Waits are bounded like a
+ * chain plan's: lk_p2p_chain_timed_out reports (and re-arms) a rank whose barrier gave up. On several
+ * GPUs the dst buffers must be coherent for peer stores (fine-grained allocations); one-GPU tests run
+ * P ranks on device 0. */
+typedef struct lk_p2p_chain lk_p2p_chain;
+int lk_p2p_chain_create(lk_p2p_group *g, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage,
+                        int n, lk_p2p_chain **out);
+/* streams[r] on rank r's device, or NULL: the group's own stream per rank, where ranks sharing a device
+ * get disjoint equal CU masks (hipExtStreamCreateWithCUMask: separate queues, every rank resident). */
+int lk_p2p_chain_launch(lk_p2p_chain *chain, void *const *streams);
+int lk_p2p_chain_timed_out(lk_p2p_chain *chain);
+uint64_t lk_p2p_chain_num_launches(const lk_p2p_chain *chain);
+void lk_p2p_chain_destroy(lk_p2p_chain *chain);
 
 /* ---- graph residency over host buffers ---------------------------------------
  * GGMLComputeOps.computeGraph / computeMulMat (core/GGMLComputeOps.kt:2515-2652) for a

@@ -347,18 +347,21 @@ int cu_count() {
 }
 
 template <int QT, int CPL>
-void launch_stream_t(int grid, const GemvDesc &single, const StreamWork *work, int spw, hipStream_t st) {
+void launch_stream_t(int grid, const GemvDesc &single, const StreamWork *work, int spw, hipStream_t st, const PeerDesc *peer) {
   constexpr size_t lds = StreamGeom<QT, CPL>::LDS;
-  hipLaunchKernelGGL((gemv_stream_kernel<QT, CPL>), dim3(grid), dim3(kStreamWaves * 64), lds, st, work, spw, single.a, single.x,
-                     single.dst, single.dst_row_stride, single.M, single.K);
+  if (peer)
+    hipLaunchKernelGGL((gemv_stream_peer_kernel<QT, CPL>), dim3(grid), dim3(kStreamWaves * 64), lds, st, work, spw, peer);
+  else
+    hipLaunchKernelGGL((gemv_stream_kernel<QT, CPL>), dim3(grid), dim3(kStreamWaves * 64), lds, st, work, spw, single.a, single.x,
+                       single.dst, single.dst_row_stride, single.M, single.K);
 }
 
 int launch_stream(int32_t qt, int cpl, int grid, const GemvDesc &single, const StreamWork *work, int spw,
-                  hipStream_t st) {
+                  hipStream_t st, const PeerDesc *peer = nullptr) {
   if (grid <= 0) return LK_OK;
-  note_route("stream<%d,%d>:g%d%s", qt, cpl, grid, work ? "p" : "");
+  note_route("stream<%d,%d>:g%d%s", qt, cpl, grid, peer ? "x" : work ? "p" : "");
 #define LK_STREAM(T, C) \
-  if (qt == T && cpl == C) { launch_stream_t<T, C>(grid, single, work, spw, st); HIP_TRY(hipGetLastError()); return LK_OK; }
+  if (qt == T && cpl == C) { launch_stream_t<T, C>(grid, single, work, spw, st, peer); HIP_TRY(hipGetLastError()); return LK_OK; }
   LK_STREAM(LK_TYPE_Q4_0, 1) LK_STREAM(LK_TYPE_Q4_0, 2) LK_STREAM(LK_TYPE_Q4_0, 3)
   LK_STREAM(LK_TYPE_Q4_1, 1) LK_STREAM(LK_TYPE_Q4_1, 2) LK_STREAM(LK_TYPE_Q4_1, 3)
   LK_STREAM(LK_TYPE_Q8_0, 1) LK_STREAM(LK_TYPE_Q8_0, 2) LK_STREAM(LK_TYPE_Q8_0, 3)
@@ -1641,6 +1644,7 @@ struct lk_plan {
   std::vector<Single> singles;
   unsigned *sync = nullptr;  // chain plans: barrier counters, exit counter, timeout flag
   int nbar = 0;
+  const PeerDesc *peer = nullptr;  // one rank of a multi-GPU chain (lk_p2p_chain): device PeerDesc
 };
 
 namespace {
@@ -1811,11 +1815,23 @@ int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
 // Chain plans: dependent stages in one launch of the streaming GEMV, one grid barrier per stage
 // boundary (gemv_stream_kernel's chain mode). One workgroup per CU, all co-resident (the
 // kernel's LDS admits one per CU).
+// Chain plan on `grid` workgroups of the current device; peer: a device PeerDesc (a rank of a
+// multi-GPU chain, lk_p2p.hip) or null.
+int lk_detail_chain_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage, int n,
+                           int grid, const void *peer, lk_plan **out);
+
 int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage, int n,
                          lk_plan **out) {
   if (!out || n <= 0 || !stage) return fail(LK_ERR_INVALID_ARG, "bad chain arguments");
   int rc = ensure_init();
   if (rc) return rc;
+  return lk_detail_chain_create(a, b, dst, stage, n, cu_count(), nullptr, out);
+}
+
+int lk_detail_chain_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage, int n,
+                           int grid, const void *peer, lk_plan **out) {
+  if (!out || n <= 0 || !stage || grid < 1) return fail(LK_ERR_INVALID_ARG, "bad chain arguments");
+  int rc = LK_OK;
   std::vector<std::vector<GemvDesc>> stages;
   int32_t qt = -1;
   int cls = 0;
@@ -1832,10 +1848,10 @@ int lk_plan_create_chain(const lk_tensor *a, const lk_tensor *b, const lk_tensor
     if ((int)stages.size() <= stage[i]) stages.emplace_back();
     stages[stage[i]].push_back(make_desc(&a[i], &b[i], &dst[i], c));
   }
-  const int grid = cu_count();
   const int nbar = (int)stages.size() - 1;
   auto plan = new lk_plan();
   plan->nbar = nbar;
+  plan->peer = (const PeerDesc *)peer;
   const size_t sync_bytes = (size_t)(nbar * 9 + 2) * kChainLine * sizeof(unsigned);
   if (hipMalloc(&plan->sync, sync_bytes) != hipSuccess || hipMemset(plan->sync, 0, sync_bytes) != hipSuccess) {
     lk_plan_destroy(plan);
@@ -1944,7 +1960,7 @@ int lk_plan_launch(lk_plan *plan, void *stream) {
   if (!plan) return fail(LK_ERR_INVALID_ARG, "null plan");
   hipStream_t st = pick_stream(stream);
   for (auto &g : plan->groups) {
-    int rc = launch_stream(g.qt, g.cls, g.grid, GemvDesc{}, g.work, g.spw, st);
+    int rc = launch_stream(g.qt, g.cls, g.grid, GemvDesc{}, g.work, g.spw, st, plan->peer);
     if (rc) return rc;
   }
   for (auto &s : plan->singles) {

@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "../../include/lk_hip.h"
+#include "lk_peer.hpp"
 
 namespace lk {
 
@@ -304,7 +305,6 @@ struct StreamWork {
 };
 static_assert(sizeof(StreamWork) == 64, "one s_load_dwordx16");
 
-constexpr int kChainLine = 32;  // chain sync words: one per 128-B line
 
 // Device-side waits (only the opt-in chain plans' grid barriers since round 4: the split-K
 // reductions elect a last arriver and never wait) are bounded: a wait that gives up counts itself
@@ -455,10 +455,19 @@ __device__ float q2k_stream_dot(uint32_t sc, const uint32_t *c, uint32_t dd, con
 // Requirements (checked by the host): K % 64 == 0, ceil(K/4096) <= CPL, row bytes
 // (K/64·PB) % 16 == 0, A and x 16-byte aligned, x contiguous. Scalar arguments only (no
 // aggregate), the work list first, so the compiler can preload them into SGPRs.
-template <int QT, int CPL>
-__global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const StreamWork *__restrict__ work, int spw,
-                                                                        const uint8_t *s_a, const float *s_x, float *s_dst,
-                                                                        int64_t s_dst_stride, int s_M, int s_K) {
+// Ranks of a multi-GPU chain (lk_p2p_chain, lk_hip.hip): one launch per rank, each a chain plan over
+// its row shards; rank `rank`'s rows are stored into its own full dst and, at dst + delta[r], into
+// every other rank's copy (system-scope write-through stores: over xGMI on a node, plain device
+// memory when ranks share a GPU). Barrier #s waits until every rank has completed stage s: the rank
+// whose top-counter add completes its stage adds 1 to cross[r] + s·kChainLine of every rank r
+// (system scope); a rank's pollers wait for its own word to reach P·(epoch + 1), where epoch counts
+// the chain's launches (the words are monotonic: a fast rank's next launch may add before a slow
+// rank has left this one, so nothing is re-armed; the rank's last workgroup out bumps its epoch).
+
+template <int QT, int CPL, bool PEER>
+__device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ work, int spw, const uint8_t *s_a,
+                                                 const float *s_x, float *s_dst, int64_t s_dst_stride, int s_M, int s_K,
+                                                 const PeerDesc *__restrict__ peer) {
   using G = StreamGeom<QT, CPL>;
   extern __shared__ f32x4 lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -476,6 +485,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const St
   const int nseg = wk ? ((const __attribute__((address_space(4))) int32_t *)wk)[offsetof(StreamWork, count) / 4] : 1;
   int nbar = 0;
   unsigned *sync = nullptr;
+  [[maybe_unused]] unsigned cross_target = 0;
+  if constexpr (PEER) {  // this launch's barriers complete at P·(epoch + 1) arrivals
+    const unsigned ep = __hip_atomic_load(peer->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cross_target = (unsigned)peer->P * (ep + 1u);
+  }
   for (int si = 0; si < nseg; si++) {
     const uint8_t *a_node;
     const float *x_node;
@@ -612,7 +626,15 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const St
         const int sh = (int)blockIdx.x % 8;
         const unsigned shn = (gridDim.x - sh + 7) / 8;  // workgroups of shard sh
         const unsigned prev = __hip_atomic_fetch_add(bsync + (1 + sh) * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == shn - 1) __hip_atomic_fetch_add(bsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == shn - 1) {
+          const unsigned top = __hip_atomic_fetch_add(bsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if constexpr (PEER) {  // this rank's stage is complete: tell every rank (itself included)
+            const unsigned nsh = gridDim.x < 8 ? gridDim.x : 8;
+            if (top == nsh - 1)
+              for (int r = 0; r < peer->P; r++)
+                __hip_atomic_fetch_add(peer->cross[r] + (bar - 1) * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
       }
       // 2. the weights do not depend on the previous stage: their stream starts now
       weight_prologue();
@@ -621,7 +643,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const St
       if (wave == 0 && lane == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), bound = lk_sync_wait_bound;
         const unsigned nsh = gridDim.x < 8 ? gridDim.x : 8;
-        while (__hip_atomic_load(bsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nsh) {
+        // PEER: this rank's cross word counts the ranks whose stage is complete (monotonic)
+        unsigned *wword = PEER ? peer->cross[PEER ? peer->rank : 0] + (bar - 1) * kChainLine : bsync;
+        const unsigned want = PEER ? cross_target : nsh;
+        while ((PEER ? __hip_atomic_load(wword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                     : __hip_atomic_load(wword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < want) {
           if (__builtin_amdgcn_s_memrealtime() - t0 >= bound) {  // not co-resident: flag it, run on
             __hip_atomic_store(sync + (nbar * 9 + 1) * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             lk_note_timeout();
@@ -778,6 +804,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const St
       if (lane == 63) {
         if (sync) __hip_atomic_store(out + (int64_t)row * dst_stride, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
         else out[(int64_t)row * dst_stride] = tot;
+        if constexpr (PEER)  // the row into every other rank's copy of dst
+          for (int r = 0; r < peer->P; r++)
+            if (r != peer->rank)
+              __hip_atomic_store((LK_GLOBAL float *)((LK_GLOBAL uint8_t *)(out + (int64_t)row * dst_stride) + peer->delta[r]), tot,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -792,10 +823,28 @@ __global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const St
       unsigned prev = 0;
       if (lane == 0) prev = __hip_atomic_fetch_add(sync + nbar * 9 * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       prev = __shfl(prev, 0, kWave);
-      if (prev == gridDim.x - 1)
+      if (prev == gridDim.x - 1) {
         for (int b = lane; b <= nbar * 9; b += kWave) __hip_atomic_store(sync + b * kChainLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (PEER)
+          if (lane == 0) __hip_atomic_fetch_add(peer->epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
+}
+
+template <int QT, int CPL>
+__global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_kernel(const StreamWork *__restrict__ work, int spw,
+                                                                        const uint8_t *s_a, const float *s_x, float *s_dst,
+                                                                        int64_t s_dst_stride, int s_M, int s_K) {
+  gemv_stream_body<QT, CPL, false>(work, spw, s_a, s_x, s_dst, s_dst_stride, s_M, s_K, nullptr);
+}
+
+// One rank of a multi-GPU chain (lk_p2p_chain): the chain-plan stream kernel with peer row stores and
+// cross-rank barriers (PeerDesc).
+template <int QT, int CPL>
+__global__ __launch_bounds__(kStreamWaves * 64) void gemv_stream_peer_kernel(const StreamWork *__restrict__ work, int spw,
+                                                                             const PeerDesc *__restrict__ peer) {
+  gemv_stream_body<QT, CPL, true>(work, spw, nullptr, nullptr, nullptr, 0, 0, 0, peer);
 }
 
 struct GenericArgs {
@@ -2186,6 +2235,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
 // Every wave issues the same DMA count per stage (CW), so a counted vmcnt plus one barrier
 // publishes a stage. Q4_0 codes carry their -8 offset ((n - 8)·2^-9, exact), so no T input.
 // Split K: each slice stores an f32 partial slab; splitk_reduce_kernel sums them in order.
+#ifndef LK_WIDE_SCHED
+#define LK_WIDE_SCHED 0  // lab builds: bit 0 scalar scale FMAs, bit 1 MFMA/VALU interleave (sched_group_barrier)
+#endif
 template <int QT> struct WideGeom {
   static constexpr int NW = 8, KG = 2, MW = NW / KG;             // waves: MW along M x KG K-groups
   static constexpr int MT = 4, NT = 4;                           // wave tile: 64 rows x 64 columns
@@ -2428,9 +2480,23 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
             f32x4 p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xl[bb][j]), wf[i],
                                                               QT == LK_TYPE_Q4_0 ? t : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             p = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xh[bb][j]), wf[i], p, 0, 0, 0);
+#if LK_WIDE_SCHED & 1
+            accumulate_s<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], p, t);
+#else
             accumulate<QT == LK_TYPE_Q4_1>(acc[i][j], s1[i], s2[i], p, t);
+#endif
           }
         }
+#if LK_WIDE_SCHED & 2
+        // the scale FMAs between the MFMAs (the compiler otherwise issues all MFMAs of the block, then
+        // all the accumulates: two waves of a SIMD in step then contend for the matrix pipe and the
+        // VALU in turn instead of overlapping them)
+#pragma unroll
+        for (int q = 0; q < MT * NT; q++) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                      // 2 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, (LK_WIDE_SCHED & 1) ? 4 : 2, 0);  // the scale FMAs
+        }
+#endif
       }
       if constexpr (!EARLY) {
         wait_lgkmcnt0();

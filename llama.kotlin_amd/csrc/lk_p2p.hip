@@ -18,12 +18,16 @@
 // queue, where a gate ahead of the push it waits for would never open).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
 #include "../../include/lk_hip.h"
+#include "lk_peer.hpp"
 
 int lk_detail_fail(int st, const char *msg);
+extern "C" int lk_detail_chain_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage,
+                                      int n, int grid, const void *peer, lk_plan **out);
 
 namespace {
 
@@ -95,6 +99,9 @@ struct lk_p2p_group {
   // once every rank's rows of that launch are in place here
   std::vector<lk_p2p_plan *> tail;
   std::vector<uint64_t> tail_target;
+  // lk_p2p_chain_launch with streams == NULL: per rank a stream of its own; ranks sharing a device
+  // get disjoint CU masks (hipExtStreamCreateWithCUMask), so they run at once on separate queues
+  std::vector<hipStream_t> rank_stream;
   uint64_t plans_alive = 0;
   bool destroyed = false;  // lk_p2p_group_destroy ran while plans were alive: the last plan deletes the group
   bool broken = false;  // a launch failed after some ranks enqueued theirs: later gates could never open
@@ -175,6 +182,14 @@ int lk_p2p_group_create(int nranks, const int *devices, lk_p2p_group **out) {
 
 int lk_p2p_group_nranks(const lk_p2p_group *g) { return g ? g->P : 0; }
 
+namespace {
+void delete_group(lk_p2p_group *g) {
+  for (size_t r = 0; r < g->rank_stream.size(); r++)
+    if (g->rank_stream[r]) (void)on_device(g->dev[r], [&] { (void)hipStreamDestroy(g->rank_stream[r]); return 0; });
+  delete g;
+}
+}  // namespace
+
 // A group with live plans is only marked: each plan holds a pointer to it, and the last plan's
 // destroy deletes it (a caller closing the group before its plans must not leave them dangling).
 void lk_p2p_group_destroy(lk_p2p_group *g) {
@@ -183,7 +198,7 @@ void lk_p2p_group_destroy(lk_p2p_group *g) {
     g->destroyed = true;
     return;
   }
-  delete g;
+  delete_group(g);
 }
 
 int lk_p2p_plan_create(lk_p2p_group *g, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
@@ -339,7 +354,217 @@ void lk_p2p_plan_destroy(lk_p2p_plan *p) {
     if (g->tail[r] == p) g->tail[r] = nullptr;  // the caller synchronized: nothing left to gate on
   g->plans_alive--;
   free_plan(p);
-  if (g->destroyed && g->plans_alive == 0) delete g;
+  if (g->destroyed && g->plans_alive == 0) delete_group(g);
+}
+
+}  // extern "C"
+
+// ---- multi-GPU chains: one persistent stream-kernel launch per rank, cross-rank barriers ------------
+//
+// lk_p2p_chain (include/lk_hip.h): the chain plan of lk_plan_create_chain (dependent stages of N = 1
+// nodes in one launch, a grid barrier between stages), per rank over its row shards, with the rows
+// stored into every rank's copy of dst and every barrier waiting for every rank's stage (PeerDesc,
+// gemv_stream_peer_kernel in lk_kernels.hpp). No host gate, no collective, no extra launch: a token's
+// whole layer stack is P concurrent launches. Ranks sharing one device (the one-GPU tests) each take
+// an equal share of its CUs and need streams of their own, since the ranks wait for each other
+// inside their launches and must therefore run at the same time.
+
+struct lk_p2p_chain {
+  lk_p2p_group *g = nullptr;
+  int nbar = 0;
+  std::vector<lk_plan *> plan;         // per rank: its chain plan (gemv_stream_peer_kernel)
+  std::vector<lk::PeerDesc *> desc;    // per rank: device copy of its PeerDesc
+  std::vector<unsigned *> cross;       // per rank: nbar arrival lines (monotonic) + the epoch line
+  uint64_t launches = 0;
+};
+
+namespace {
+
+void free_chain(lk_p2p_chain *c) {
+  for (int r = 0; r < (int)c->plan.size(); r++) {
+    (void)on_device(c->g->dev[r], [&] {
+      if (c->plan[r]) lk_plan_destroy(c->plan[r]);
+      if (c->desc[r]) (void)hipFree(c->desc[r]);
+      if (c->cross[r]) (void)hipFree(c->cross[r]);
+      return 0;
+    });
+  }
+  delete c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lk_p2p_chain_create(lk_p2p_group *g, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage,
+                        int n, lk_p2p_chain **out) {
+  if (!g || !out || n <= 0 || !a || !b || !dst || !stage) return lk_detail_fail(LK_ERR_INVALID_ARG, "p2p chain: bad arguments");
+  *out = nullptr;
+  const int P = g->P;
+  if (P > lk::kMaxPeerRanks) return lk_detail_fail(LK_ERR_INVALID_ARG, "p2p chain: at most 8 ranks");
+  // every rank's dst of node i: one shape, dense rows, M % P == 0, and one byte offset per rank
+  // between rank q's dst and rank r's over all nodes (the kernel stores rank r's rows at dst + delta)
+  std::vector<int64_t> delta((size_t)P * P, 0);
+  for (int i = 0; i < n; i++) {
+    const lk_tensor &d0 = dst[i];
+    for (int r = 0; r < P; r++) {
+      const lk_tensor &d = dst[r * n + i];
+      const int64_t M = d.ne[1];
+      if (d.type != LK_TYPE_F32 || d.ne[0] != 1 || d0.ne[1] != M || d.nb[1] != 4 || !d.data)
+        return lk_detail_fail(LK_ERR_INVALID_ARG, "p2p chain: every dst must be a dense F32 [1, M], one shape per node");
+      if (M % P != 0 || a[r * n + i].ne[1] != M / P)
+        return lk_detail_fail(LK_ERR_INVALID_ARG, "p2p chain: A must hold rows [r*M/P, (r+1)*M/P) with M % P == 0");
+      if (d.data_offset + (uint64_t)M * 4 > d.buf_bytes) return lk_detail_fail(LK_ERR_OUT_OF_BOUNDS, "p2p chain: dst exceeds its buffer");
+      for (int q = 0; q < P; q++) {
+        const lk_tensor &dq = dst[q * n + i];
+        const int64_t dl = (int64_t)((uintptr_t)d.data + d.data_offset) - (int64_t)((uintptr_t)dq.data + dq.data_offset);
+        if (i == 0) delta[(size_t)q * P + r] = dl;
+        else if (delta[(size_t)q * P + r] != dl)
+          return lk_detail_fail(LK_ERR_NOT_IMPLEMENTED, "p2p chain: each rank's dst tensors must share one layout (one offset per rank pair)");
+      }
+    }
+  }
+  int nstage = 0;
+  for (int i = 0; i < n; i++) nstage = std::max(nstage, stage[i] + 1);
+  auto c = new lk_p2p_chain();
+  c->g = g;
+  c->nbar = nstage - 1;
+  c->plan.assign(P, nullptr);
+  c->desc.assign(P, nullptr);
+  c->cross.assign(P, nullptr);
+  // ranks per device: they share its CUs (all of a rank's workgroups and every other rank's must be
+  // resident at once: a barrier waits for every rank)
+  std::vector<int> share(P, 0);
+  for (int r = 0; r < P; r++)
+    for (int q = 0; q < P; q++) share[r] += g->dev[q] == g->dev[r];
+  const size_t lines = (size_t)std::max(c->nbar, 1) + 1;  // barrier lines + the epoch line
+  for (int r = 0; r < P; r++) {
+    const int rc = on_device(g->dev[r], [&]() -> int {
+      if (hipMalloc((void **)&c->cross[r], lines * lk::kChainLine * sizeof(unsigned)) != hipSuccess) {
+        c->cross[r] = nullptr;
+        return lk_detail_fail(LK_ERR_DEVICE, "p2p chain: out of device memory");
+      }
+      if (hipMemset(c->cross[r], 0, lines * lk::kChainLine * sizeof(unsigned)) != hipSuccess)
+        return lk_detail_fail(LK_ERR_DEVICE, "p2p chain: cannot zero the arrival words");
+      return (int)LK_OK;
+    });
+    if (rc) { free_chain(c); return rc; }
+  }
+  for (int r = 0; r < P; r++) {
+    lk::PeerDesc pd;
+    std::memset(&pd, 0, sizeof pd);
+    pd.P = P;
+    pd.rank = r;
+    for (int q = 0; q < P; q++) {
+      pd.delta[q] = delta[(size_t)r * P + q];
+      pd.cross[q] = c->cross[q];
+    }
+    pd.epoch = c->cross[r] + (lines - 1) * lk::kChainLine;
+    // this rank's nodes: its row shard of A, its copy of B, its rows inside its full dst
+    std::vector<lk_tensor> la(a + r * n, a + (r + 1) * n), lb(b + r * n, b + (r + 1) * n), ld(dst + r * n, dst + (r + 1) * n);
+    for (int i = 0; i < n; i++) {
+      const int64_t rows = ld[i].ne[1] / P;
+      ld[i].ne[1] = rows;
+      ld[i].data_offset += (uint64_t)r * rows * 4;
+    }
+    const int rc = on_device(g->dev[r], [&]() -> int {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->dev[r]) != hipSuccess || cus <= 0) cus = 256;
+      const int grid = std::max(1, cus / share[r]);
+      if (hipMalloc((void **)&c->desc[r], sizeof pd) != hipSuccess) {
+        c->desc[r] = nullptr;
+        return lk_detail_fail(LK_ERR_DEVICE, "p2p chain: out of device memory");
+      }
+      if (hipMemcpy(c->desc[r], &pd, sizeof pd, hipMemcpyHostToDevice) != hipSuccess)
+        return lk_detail_fail(LK_ERR_DEVICE, "p2p chain: upload failed");
+      return lk_detail_chain_create(la.data(), lb.data(), ld.data(), stage, n, grid, c->desc[r], &c->plan[r]);
+    });
+    if (rc) { free_chain(c); return rc; }
+  }
+  g->plans_alive++;
+  *out = c;
+  return LK_OK;
+}
+
+namespace {
+// The group's own per-rank streams (created once): ranks sharing a device get disjoint, equal CU masks.
+int rank_streams(lk_p2p_group *g) {
+  if (!g->rank_stream.empty()) return LK_OK;
+  const int P = g->P;
+  std::vector<hipStream_t> st(P, nullptr);
+  for (int r = 0; r < P; r++) {
+    int share = 0, idx = 0;
+    for (int q = 0; q < P; q++) {
+      share += g->dev[q] == g->dev[r];
+      idx += q < r && g->dev[q] == g->dev[r];
+    }
+    const int rc = on_device(g->dev[r], [&]() -> int {
+      if (share == 1) return hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking) == hipSuccess ? (int)LK_OK
+                                                                                                  : lk_detail_fail(LK_ERR_DEVICE, "p2p chain: stream");
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->dev[r]) != hipSuccess || cus <= 0)
+        return lk_detail_fail(LK_ERR_DEVICE, "p2p chain: CU count");
+      const int per = cus / share;
+      std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+      for (int cu = idx * per; cu < (idx + 1) * per; cu++) mask[cu / 32] |= 1u << (cu % 32);
+      return hipExtStreamCreateWithCUMask(&st[r], (uint32_t)mask.size(), mask.data()) == hipSuccess
+                 ? (int)LK_OK : lk_detail_fail(LK_ERR_DEVICE, "p2p chain: CU-masked stream");
+    });
+    if (rc) {
+      for (int q = 0; q < r; q++) (void)on_device(g->dev[q], [&] { (void)hipStreamDestroy(st[q]); return 0; });
+      return rc;
+    }
+  }
+  g->rank_stream = st;
+  return LK_OK;
+}
+}  // namespace
+
+int lk_p2p_chain_launch(lk_p2p_chain *c, void *const *streams) {
+  if (!c) return lk_detail_fail(LK_ERR_INVALID_ARG, "p2p chain: null chain");
+  lk_p2p_group *g = c->g;
+  const int P = g->P;
+  std::vector<void *> own;
+  if (!streams) {  // the group's per-rank streams (CU-partitioned where ranks share a device)
+    if (int rc = rank_streams(g)) return rc;
+    own.assign(g->rank_stream.begin(), g->rank_stream.end());
+    streams = own.data();
+  }
+  for (int r = 0; r < P; r++)
+    for (int q = 0; q < r; q++)
+      if (g->dev[q] == g->dev[r] && streams[q] == streams[r])
+        return lk_detail_fail(LK_ERR_INVALID_ARG, "p2p chain: ranks on one device need streams of their own (they run at once)");
+  if (g->broken) return lk_detail_fail(LK_ERR_DEVICE, "p2p chain: an earlier launch in this group failed part-way");
+  for (int r = 0; r < P; r++) {
+    const int rc = on_device(g->dev[r], [&]() -> int { return lk_plan_launch(c->plan[r], streams[r]); });
+    if (rc) {  // ranks before r wait at their first barrier for this one: they give up at the bound
+      g->broken = true;
+      return rc;
+    }
+  }
+  c->launches++;
+  return LK_OK;
+}
+
+int lk_p2p_chain_timed_out(lk_p2p_chain *c) {
+  if (!c) return lk_detail_fail(LK_ERR_INVALID_ARG, "p2p chain: null chain");
+  int any = 0;
+  for (int r = 0; r < c->g->P; r++) {
+    const int rc = on_device(c->g->dev[r], [&]() -> int { return lk_plan_chain_timed_out(c->plan[r]); });
+    if (rc < 0 || rc > 1) return rc;
+    any |= rc;
+  }
+  return any;
+}
+
+uint64_t lk_p2p_chain_num_launches(const lk_p2p_chain *c) { return c ? c->launches : 0; }
+
+void lk_p2p_chain_destroy(lk_p2p_chain *c) {
+  if (!c) return;
+  lk_p2p_group *g = c->g;
+  g->plans_alive--;
+  free_chain(c);
+  if (g->destroyed && g->plans_alive == 0) delete_group(g);
 }
 
 }  // extern "C"

@@ -22,7 +22,7 @@ from .ops import (DotKind, MulMatPlan, ResidentGraph, computeDotProductF32Q41, c
                   computeMatMulSharded, dequantizeTensor, quantizeTensor, setSyncWaitBound, syncCountersSum, syncTimeouts, debugRoute, debugScratchEpoch, to_lk, validateMatMul, weightsCachedBytes, weightsCachedCount,
                   weightsEvict, weightsEvictAll, weightsEvictBuffer, weightsPin, weightsPinSharded)
 from .gguf import GGUFContext, GGUFParser, GGUFTensorInfo, GGUFType, LoadedModel, ModelLoader
-from .sharded import Comm, P2PGroup, P2PMulMatPlan, RowShardedMulMat, ShardedMulMatPlan, row_slice, shard_rows, shard_view
+from .sharded import Comm, P2PChain, P2PGroup, P2PMulMatPlan, RowShardedMulMat, ShardedMulMatPlan, row_slice, shard_rows, shard_view
 from .tensor import (GGMLCGraph, GGMLContext, GGMLGraphAllocator, GGMLOp, GGMLTensor, GGMLType,
                      calculateContiguousStrides, calculateTensorByteSize)
 
@@ -35,7 +35,7 @@ __all__ = [
     "computeDotProductF32Q80", "computeDotProductQ80Q80", "computeDotProductQ40Q40", "computeDotProductQ41Q41",
     "computeDotProductQ80Q40",
     "GGMLHipBackend", "GGMLStatus", "GGMLBackendRegistry",
-    "RowShardedMulMat", "row_slice", "shard_rows", "Comm", "ShardedMulMatPlan", "shard_view", "P2PGroup", "P2PMulMatPlan",
+    "RowShardedMulMat", "row_slice", "shard_rows", "Comm", "ShardedMulMatPlan", "shard_view", "P2PGroup", "P2PMulMatPlan", "P2PChain",
     "GGUFParser", "GGUFContext", "GGUFTensorInfo", "GGUFType", "ModelLoader", "LoadedModel",
     "IllegalArgumentException", "IndexOutOfBoundsException", "IllegalStateException", "NotOffloadedError",
     "HipDeviceError",

@@ -89,6 +89,8 @@ EXPORTED_SYMBOLS = (
     "lk_sharded_plan_create", "lk_sharded_plan_launch", "lk_sharded_plan_num_gathers", "lk_sharded_plan_destroy",
     "lk_p2p_group_create", "lk_p2p_group_nranks", "lk_p2p_group_destroy", "lk_p2p_plan_create", "lk_p2p_plan_launch",
     "lk_p2p_plan_num_launches", "lk_p2p_plan_signal", "lk_p2p_plan_destroy",
+    "lk_p2p_chain_create", "lk_p2p_chain_launch", "lk_p2p_chain_timed_out", "lk_p2p_chain_num_launches",
+    "lk_p2p_chain_destroy",
     "lk_dequantize_device", "lk_quantize_device", "lk_dot_direct", "lk_dot_direct_device",
     # include/lk_gguf.h
     "lk_gguf_open_memory", "lk_gguf_open_file", "lk_gguf_close", "lk_gguf_version", "lk_gguf_alignment",
@@ -191,6 +193,14 @@ def load():
         L.lk_p2p_plan_signal.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         L.lk_p2p_plan_destroy.argtypes = [vp]
         L.lk_p2p_plan_destroy.restype = None
+    if hasattr(L, "lk_p2p_chain_create"):  # (absent from round-4 lab builds loaded for A/B)
+        L.lk_p2p_chain_create.argtypes = [vp, P, P, P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.POINTER(vp)]
+        L.lk_p2p_chain_launch.argtypes = [vp, ctypes.c_void_p]
+        L.lk_p2p_chain_timed_out.argtypes = [vp]
+        L.lk_p2p_chain_num_launches.argtypes = [vp]
+        L.lk_p2p_chain_num_launches.restype = ctypes.c_uint64
+        L.lk_p2p_chain_destroy.argtypes = [vp]
+        L.lk_p2p_chain_destroy.restype = None
     L.lk_dequantize_device.argtypes = [P, vp, vp]
     L.lk_quantize_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp]
     L.lk_dot_direct.argtypes = [ctypes.c_int32, P, P, ctypes.c_int64, vp]

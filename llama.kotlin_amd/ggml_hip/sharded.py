@@ -335,3 +335,72 @@ class P2PMulMatPlan:
             self.close()
         except Exception:
             pass
+
+
+class P2PChain:
+    """lk_p2p_chain: dependent stages of N = 1 MUL_MAT nodes (a model's layers) as ONE persistent
+    launch per rank. ``ranks[r]`` = [(a_shard, b, dst_full)] for rank r — its row shard of each node's
+    weights, its copy of the activations (for a later stage: its copy of an earlier node's dst), its
+    full dst; every rank's dst tensors laid out alike. ``stages``: one stage id per node (0, then
+    non-decreasing by at most 1). A launch streams every rank's rows, stores each into every rank's
+    dst and waits, between stages, for every rank (no collective, no host gate)."""
+
+    def __init__(self, group: P2PGroup, ga, ranks, stages):
+        import ctypes
+        from . import _lib
+        from .ops import to_lk
+        P = group.nranks
+        if len(ranks) != P or len({len(nodes) for nodes in ranks}) != 1:
+            raise ValueError("one node list of equal length per rank")
+        gas = ga if isinstance(ga, (list, tuple)) else [ga] * P
+        n = len(ranks[0])
+        if len(stages) != n:
+            raise _lib.IllegalArgumentException("one stage id per node")
+        A = (_lib.LkTensor * max(P * n, 1))()
+        B = (_lib.LkTensor * max(P * n, 1))()
+        D = (_lib.LkTensor * max(P * n, 1))()
+        for r, nodes in enumerate(ranks):
+            for i, (a, b, d) in enumerate(nodes):
+                A[r * n + i], B[r * n + i], D[r * n + i] = to_lk(gas[r], a), to_lk(gas[r], b), to_lk(gas[r], d)
+        S = (ctypes.c_int32 * max(n, 1))(*[int(v) for v in stages])
+        self._handle = ctypes.c_void_p()
+        _lib.check(_lib.load().lk_p2p_chain_create(group._handle, A, B, D, S, n, ctypes.byref(self._handle)))
+        self.group = group
+        self._keep = (A, B, D, S)
+
+    def launch(self, streams=None):
+        """``streams``: one torch stream per rank (ranks on one device: distinct streams that can run
+        at once), or None: the group's own per-rank streams (CU-partitioned where ranks share a GPU)."""
+        import ctypes
+        from . import _lib
+        if streams is None:
+            _lib.check(_lib.load().lk_p2p_chain_launch(self._handle, None))
+            return
+        P = self.group.nranks
+        hs = (ctypes.c_void_p * P)(*[int(s.cuda_stream) for s in streams])
+        _lib.check(_lib.load().lk_p2p_chain_launch(self._handle, hs))
+
+    def timedOut(self) -> bool:
+        """True if any rank's barrier gave up waiting (synchronizes the ranks' devices; re-arms)."""
+        from . import _lib
+        st = _lib.load().lk_p2p_chain_timed_out(self._handle)
+        if st < 0 or st > 1:
+            _lib.check(st)
+        return st == 1
+
+    @property
+    def numLaunches(self) -> int:
+        from . import _lib
+        return int(_lib.load().lk_p2p_chain_num_launches(self._handle))
+
+    def close(self):
+        if self._handle:
+            from . import _lib
+            _lib.load().lk_p2p_chain_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
