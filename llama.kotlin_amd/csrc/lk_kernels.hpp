@@ -1907,7 +1907,11 @@ template <int QT, int NT> struct SkinnyPairGeom {
   static constexpr int SB = 16, SBH = 8;                // blocks per slice / per half
   static constexpr int RPH = SBH * BB;                  // bytes of a half row piece (multiple of 16)
   static constexpr int PPH = RPH / 16;                  // 16-B cells per half row
-  static constexpr int L = (16 * PPH + 63) / 64;        // DMA instructions per half unit
+  // cells per LDS row: odd, so the 16 rows of a unit start on 16 distinct 4-bank groups (Q4_1's
+  // 10 cells would put rows m and m + 8 on the same banks: 2-way conflicts on every weight read)
+  static constexpr int CPR = PPH | 1;
+  static constexpr int PITCH = CPR * 16;                // LDS row pitch
+  static constexpr int L = (16 * CPR + 63) / 64;        // DMA instructions per half unit
   static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
   static constexpr int SLOT = L * 1024;
   static constexpr int XB = SB * NT * kXSplits * 1024;  // activation fragments (staging)
@@ -2027,13 +2031,13 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   const int myL = nbh > 0 ? L : 0;
 
   // half unit u = rows of tile t0 + p + 4u, bytes [kb0·BB + h·RPH, + nbh·BB) of each; cell
-  // q = r·PPH + c lands at slot + 16q (row pitch RPH); cells past the unit re-read cell 0
+  // q = r·CPR + c lands at slot + 16q (row pitch PITCH); pad cells and cells past the unit re-read cell 0
   const uint8_t *abase = g.a + (int64_t)kb0 * BB + (int64_t)h * G::RPH;
   uint32_t rofs[L];
   int rrow[L];
 #pragma unroll
   for (int j = 0; j < L; j++) {
-    const int q = j * 64 + lane, r = q / G::PPH, c = q % G::PPH;
+    const int q = j * 64 + lane, r = q / G::CPR, c = q % G::CPR;
     rrow[j] = min(r, 15);
     rofs[j] = (uint32_t)((c < pph && r < 16) ? c * 16 : 0);
   }
@@ -2151,7 +2155,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       uint32_t wd[8][G::WPB];
       const uint8_t *slot_ptr = ring + slot * G::SLOT;
       {
-        const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::RPH;
+        const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::PITCH;
         const uint8_t *bg = bm + (QT == LK_TYPE_Q8_0 ? 8 : 4) * (lane >> 4);
         skinny_read_all<QT, 8, G::WPB, 0>(bm, bg, wd);
         asm volatile("" ::: "memory");
@@ -2162,7 +2166,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
         // acc += Σ_b e_b(row)·T_b(column) over the half's 8 blocks, two f32 MFMAs (K = 4 blocks)
         // per 16-column tile: e = d (Q4_0, T = −136·Σ(hi + lo)) or m (Q4_1, T = Σx); lane
         // (m = lane & 15, b' = lane >> 4) reads its row's header of block 4c + b'
-        const uint8_t *hrow = slot_ptr + (lane & 15) * G::RPH;
+        const uint8_t *hrow = slot_ptr + (lane & 15) * G::PITCH;
 #pragma unroll
         for (int c = 0; c < 2; c++) {
           const int bl = 4 * c + (lane >> 4);

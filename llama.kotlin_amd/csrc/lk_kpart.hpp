@@ -60,7 +60,11 @@ template <int QT, int NT> struct KpartGeom {
   static constexpr int SPAN = NW * KB;                // blocks per workgroup (one K slice)
   static constexpr int PIECE = KB * BB;               // bytes of a wave's row piece
   static constexpr int PP = PIECE / 16;               // its 16-B cells
-  static constexpr int L = (16 * PP + 63) / 64;       // DMA instructions per unit (16 rows)
+  // cells per LDS row: odd, so the 16 rows of a unit start on 16 distinct 4-bank groups (Q4_1's
+  // 10 cells would put rows m and m + 8 on the same banks: 2-way conflicts on every weight read)
+  static constexpr int CP = PP | 1;
+  static constexpr int PITCH = CP * 16;               // LDS row pitch
+  static constexpr int L = (16 * CP + 63) / 64;       // DMA instructions per unit (16 rows)
   static constexpr int SLOT = L * 1024;
   static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : 3;
   static constexpr int NB = 4;                        // tile slots (tiles in flight in the workgroup)
@@ -195,14 +199,14 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
   // counts 0; done[s] = s − NB: slot s first holds unit s, with no predecessor to wait for
   if (threadIdx.x < 2 * NB) ldsk_st((LK_LDS int *)cnt + threadIdx.x, threadIdx.x < NB ? 0 : (int)threadIdx.x - 2 * NB);
 
-  // unit u = rows of tile t0 + u, bytes [kbw·BB, + nbw·BB) of each; cell q = r·PP + c lands at
-  // slot + 16q (row pitch PIECE); cells past the unit re-read cell 0
+  // unit u = rows of tile t0 + u, bytes [kbw·BB, + nbw·BB) of each; cell q = r·CP + c lands at
+  // slot + 16q (row pitch PITCH); pad cells and cells past the unit re-read cell 0
   const uint8_t *abase = g.a + (int64_t)kbw * BB;
   uint32_t rofs[L];
   int rrow[L];
 #pragma unroll
   for (int j = 0; j < L; j++) {
-    const int q = j * 64 + lane, r = q / G::PP, c = q % G::PP;
+    const int q = j * 64 + lane, r = q / G::CP, c = q % G::CP;
     rrow[j] = min(r, 15);
     rofs[j] = (uint32_t)((c < pp && r < 16) ? c * 16 : 0);
   }
@@ -386,7 +390,7 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
       uint32_t wd[KB][G::WPB];
       const uint8_t *slot_ptr = ring + slot * G::SLOT;
       {
-        const uint8_t *bm = slot_ptr + (lane & 15) * G::PIECE;
+        const uint8_t *bm = slot_ptr + (lane & 15) * G::PITCH;
         const uint8_t *bg = bm + 4 * (lane >> 4);
         skinny_read_all<QT, KB, G::WPB, 0>(bm, bg, wd);
         asm volatile("" ::: "memory");
@@ -395,7 +399,7 @@ __global__ __launch_bounds__(512) void gemm_kpart_kernel(KpartArgs g) {
       else kpart_blocks<QT, NT, KB, G::WPB, false, 0>(wd, nbw, xh, xl, acc);
       // acc += Σ_b e_b(row)·T_b(column), K = 4 blocks per f32 MFMA: e = d (Q4_0, T = −136·Σ(hi + lo))
       // or m (Q4_1, T = Σx); lane (m = lane & 15, b' = lane >> 4) reads its row's header of 4c + b'
-      const uint8_t *hrow = slot_ptr + (lane & 15) * G::PIECE;
+      const uint8_t *hrow = slot_ptr + (lane & 15) * G::PITCH;
 #pragma unroll
       for (int c = 0; c < KB / 4; c++) {
         const int bl = 4 * c + (lane >> 4);

@@ -76,6 +76,8 @@ def main():
     if "skinny" in want:
         out["q4_0_n8"] = _single(torch, G, dev, s, T.Q4_0, 11008, 4096, 8, 16)
         out["q4_0_n16"] = _single(torch, G, dev, s, T.Q4_0, 11008, 4096, 16, 16)
+    if "skinny41" in want:
+        out["q4_1_n16"] = _single(torch, G, dev, s, T.Q4_1, 11008, 4096, 16, 16)
     if "c1" in want:
         out["c1_f32"] = _single(torch, G, dev, s, T.F32, 512, 512, 512, 4)
     if "down32" in want:
