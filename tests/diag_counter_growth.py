@@ -5,8 +5,11 @@ tests/test_graph_gpu.py (Q4_0, K = 384: 216-B rows, so gemm_q_mfma_kernel with 1
 arrival counter per 128-row tile) with the row count growing call by call, so every call needs more
 tile counters than exist: round 4's library reallocated them each time (hipFree + hipMalloc + a
 hipMemset on the null stream, which nothing orders before a launch on a non-blocking stream); round 5
-zeroes them with hipMemsetAsync on the launch stream. Every result against the oracle; prints one line
-per call that misses the parity bar and a summary. Usage: [LK_HIP_LIB=...] python tests/diag_counter_growth.py"""
+zeroes them with hipMemsetAsync on the launch stream. BUSY=1 first queues ~10 ms of torch matmuls on torch's default
+stream — the legacy null stream, behind which round 4's hipMemset waits while the library's
+non-blocking stream runs the kernel at once. Every result against the oracle; prints one line
+per call that misses the parity bar and a summary.
+Usage: [LK_HIP_LIB=...] [BUSY=1] python tests/diag_counter_growth.py"""
 import os
 import sys
 
@@ -28,6 +31,9 @@ def main():
     torch.cuda.set_device(0)
     K, N = 384, 4
     bad = 0
+    busy = os.environ.get("BUSY") == "1"
+    sq = torch.randn(2048, 2048, device="cuda") / 64
+    torch.cuda.synchronize()
     for rep in range(int(os.environ.get("REPS", "3"))):
         for t in range(1, 41):
             M = 128 * t + 128 * 40 * rep  # more tiles than any call before
@@ -37,6 +43,10 @@ def main():
             junk = torch.full((1 << 18,), -1, dtype=torch.int32, device="cuda")
             del junk
             torch.cuda.empty_cache()
+            if busy:  # the null stream busy for ~10 ms (not waited for)
+                y = sq
+                for _ in range(60):
+                    y = y @ sq
             got = gpu_matmul(2, q, M, K, N, x, host=True)
             ref = O.mat_mul_q(2, q, M, K, x)
             ok, msg = parity_ok(got, ref, noise=noise_for(O, 2, q, M, K, x))
@@ -44,8 +54,9 @@ def main():
                 bad += 1
                 err = np.abs(got - ref).max(axis=1)
                 rows = np.nonzero(err > 1e-3 * np.abs(ref).max())[0]
+                zeros = int((got == 0).sum())
                 print(f"rep {rep} M {M}: {msg}; wrong rows {rows.min()}..{rows.max()} ({rows.size}) "
-                      f"tiles {sorted(set((rows // 128).tolist()))[:8]}", flush=True)
+                      f"tiles {sorted(set((rows // 128).tolist()))[:8]} exact zeros {zeros} of {got.size}", flush=True)
     print(f"calls off the oracle: {bad} of {40 * int(os.environ.get('REPS', '3'))}", flush=True)
 
 

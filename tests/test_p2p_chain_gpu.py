@@ -38,9 +38,10 @@ def _nodes(w, t, layers, a_of):
     nodes, stages = [], []
     for L in range(layers):
         for (name, m, k, src) in LAYER:
-            b = t[f"x{L}"] if src == "x" else t[f"{src}{L}"]
-            if src == "x" and L > 0:
-                b = t[f"down{L - 1}"]
+            if src == "x":  # layer L reads the previous layer's down projection
+                b = t["x0"] if L == 0 else t[f"down{L - 1}"]
+            else:
+                b = t[f"{src}{L}"]
             nodes.append((a_of(w[f"{name}{L}"]), b, t[f"{name}{L}"]))
             stages.append(4 * L + STAGE_OF[name])
     return nodes, stages

@@ -169,3 +169,41 @@ def test_concurrent_streams_do_not_share_scratch(gpu, oracle):
         ok, msg = parity_ok(got, refs[1], noise=noise[1])
         assert ok, (j, msg)
     assert G.syncCountersSum() == 0
+
+
+def test_counter_growth_behind_a_busy_null_stream(gpu, oracle):
+    """Round 4's resident-graph failure, built directly: round 4 zeroed newly grown tile
+    counters with hipMemset on the null stream, which the library's non-blocking stream does not wait
+    for. With torch's default (null) stream busy, the GEMM could run on unzeroed (recycled) counter
+    words: on such a tile no slice saw itself last, so its outputs were never written (exact zeros).
+    Host-path calls of the graph test's down-projection shape (gemm_q_*: 12 K slices, a counter per
+    tile), each queued behind ~10 ms of torch work on the default stream, the last one growing the
+    counters past their 4096-tile floor (hipMemsetAsync on the launch stream since round 5)."""
+    import torch
+    import ggml_hip as G
+    K, N, RB = 384, 4, 384 // 32 * 18
+    sq = torch.randn(2048, 2048, device="cuda") / 64
+    grew = False
+    for M in (256, 128 * 40, 128 * 4097 + 64):
+        q = oracle.quantize(2, random_weights(M * K, M % 1000))
+        x = random_acts(K * N, M % 1000 + 1).reshape(K, N)
+        junk = torch.full((1 << 22,), -1, dtype=torch.int32, device="cuda")  # recycled memory is not zero
+        del junk
+        torch.cuda.empty_cache()
+        torch.cuda.synchronize()
+        y = sq
+        for _ in range(60):  # the null stream busy; nothing waits for it
+            y = y @ sq
+        e0 = G.debugScratchEpoch()
+        G.debugRoute()
+        got = gpu_matmul(2, q, M, K, N, x, host=True)
+        route = G.debugRoute()
+        grew |= G.debugScratchEpoch() > e0
+        assert "gemm_q_" in route, route
+        assert not any((got[t:t + 64] == 0).all() for t in range(0, M, 64)), (M, route)  # no unwritten tile
+        rows = np.unique(np.concatenate([np.arange(0, M, 97), [M - 1]]))  # rows of every tile
+        qs = np.ascontiguousarray(q.reshape(M, RB)[rows]).reshape(-1)
+        _check_oracle(oracle, 2, qs, rows.size, K, x, got[rows])
+    torch.cuda.synchronize()
+    assert grew, "no call grew the scratch"
+    assert G.syncCountersSum() == 0

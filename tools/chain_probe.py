@@ -4,6 +4,8 @@ launches, over Llama-7B layers in the dependent decode order (4 stages per layer
 ranks split its CUs, so the bytes per stage and the CUs streaming them are those of the single-rank
 chain: what changes is the barrier (every rank's stage, announced to every rank) and the row stores
 into P copies. One JSON line: us per layer for each form, eager launches timed between events.
+Both chains are also timed by host wall clock around launch + synchronize (`*_wall_*`: includes one
+launch and one synchronize per rep, the only clock that spans every rank's stream).
 Usage: python tools/chain_probe.py [layers]"""
 import json
 import os
@@ -18,7 +20,7 @@ import bench  # noqa: E402
 def main():
     import torch
     import ggml_hip as G
-    layers = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    layers = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     T = G.GGMLType
@@ -78,11 +80,23 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / reps / layers
 
+    import time
+
+    def wall(fn, reps=10):  # launch + synchronize per rep: the form the multi-rank chain is timed in
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+            torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e6 / reps / layers
+
     # stream-ordered: one plan per stage
     plans = [G.MulMatPlan(ga, [n for n, st in zip(nodes, stages) if st == k]) for k in range(max(stages) + 1)]
     out["stream_ordered_us_per_layer"] = round(timed(lambda: [p.launch(stream=s) for p in plans]), 3)
     chain = G.MulMatPlan(ga, nodes, stages=stages)
     out["chain_plan_us_per_layer"] = round(timed(lambda: chain.launch(stream=s)), 3)
+    out["chain_plan_wall_us_per_layer"] = round(wall(lambda: chain.launch(stream=s)), 3)
     out["chain_plan_timed_out"] = chain.timedOut()
     for P in (1, 2, 4):
         ranks = []
@@ -96,15 +110,8 @@ def main():
 
         def run():
             pc.launch()  # the group's CU-partitioned streams
-            torch.cuda.synchronize()
 
-        run()
-        import time
-        t0 = time.perf_counter()
-        reps = 10
-        for _ in range(reps):
-            run()
-        out[f"p2p_chain_P{P}_us_per_layer"] = round((time.perf_counter() - t0) * 1e6 / reps / layers, 3)
+        out[f"p2p_chain_P{P}_wall_us_per_layer"] = round(wall(run), 3)
         out[f"p2p_chain_P{P}_timed_out"] = pc.timedOut()
         last = ranks[-1][-1][2]
         ref = t1[(layers - 1, "down")]
