@@ -545,6 +545,10 @@ int launch_gemm_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
   int slices = std::max(1, std::min({(gemm_occupancy() * cu_count() + tiles - 1) / tiles, 32, nblk}));
   g.kslice = (nblk + slices - 1) / slices;
   slices = (nblk + g.kslice - 1) / g.kslice;
+  if ((size_t)slices * tiles * BM * BN * sizeof(float) >= (1ull << 31)) {  // slabs through a 32-bit buffer offset
+    g.kslice = nblk;
+    slices = 1;
+  }
   g.slices = slices;
   if (slices > 1) {
     int rc = grow(S, &S.partial, &S.partial_bytes, (size_t)slices * tiles * BM * BN * sizeof(float));
@@ -583,6 +587,10 @@ int launch_gemm_lds_t(GemmArgs g, const XSplitArgs &xa, hipStream_t st) {
   int slices = std::max(1, std::min({(gemm_occupancy() * cu_count() / 4 + tiles - 1) / tiles, 32, nst}));
   g.kslice = ((nst + slices - 1) / slices) * GG::SB;
   slices = (g.K / 32 + g.kslice - 1) / g.kslice;
+  if ((size_t)slices * tiles * GG::BM * GG::BN * sizeof(float) >= (1ull << 31)) {  // slabs through a 32-bit buffer offset
+    g.kslice = g.K / 32;
+    slices = 1;
+  }
   g.slices = slices;
   if (slices > 1) {
     int rc = grow(S, &S.partial, &S.partial_bytes, (size_t)slices * tiles * GG::BM * GG::BN * sizeof(float));

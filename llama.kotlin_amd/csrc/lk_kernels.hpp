@@ -1079,6 +1079,8 @@ __device__ __forceinline__ void accumulate_s(f32x4 &acc, float s1, float s2, f32
   acc.z = fmaf(s1, p.z, acc.z); acc.w = fmaf(s1, p.w, acc.w);
 }
 
+__device__ __forceinline__ bool splitk_arrive(unsigned *cnt, unsigned slices);  // below
+
 // Epilogue shared by the GEMM kernels: lane holds C'(n = 16·xtile + 4(lane>>4) + e, m = row),
 // e = 0..3. slices == 1: store. Split-K: publish this slice's tile; the last slice to arrive sums
 // all slices in slice order (deterministic) and stores, then re-arms the tile counter.
@@ -1106,33 +1108,41 @@ __device__ __forceinline__ void gemm_finish(const GemmArgs &g, f32x4 (&acc)[MT][
       for (int j = 0; j < NT; j++) store(i, j, acc[i][j]);
     return;
   }
+  // The tile's slab rows are handed to the last arriver by hand-off row 1 of MI355X_MICROARCH.md
+  // (as splitk_arrive for the other kernels): written through (sc1), every wave's stores drained
+  // (vmcnt(0)), a workgroup barrier, then one lane's agent-scope add; the last arriver reads the
+  // slabs with sc1 loads and re-arms the counter with an atomic store. Round 4 published them with
+  // plain stores behind per-thread __threadfence(), read them back with plain loads and re-armed the
+  // counter with a plain store — none of the guide's validated forms.
   const int tile_elems = BM * BN;
   const int lin0 = wave * MT * NT * 256;  // wave-local layout: [wave][i][j][lane][4]
-  float *mine = g.partial + ((int64_t)slice * tiles + tile) * tile_elems;
+  const int64_t pbytes = (int64_t)g.slices * tiles * tile_elems * 4;  // < 2^31 (host-checked)
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, (int)pbytes, 0x00020000);
+  auto at = [&](int sl, int i, int j) __attribute__((always_inline)) {  // byte offset of a lane's f32x4
+    return (int)(((((int64_t)sl * tiles + tile) * tile_elems) + lin0 + (i * NT + j) * 256 + 4 * lane) * 4);
+  };
 #pragma unroll
   for (int i = 0; i < MT; i++)
 #pragma unroll
-    for (int j = 0; j < NT; j++) ((f32x4 *)mine)[(lin0 + (i * NT + j) * 256) / 4 + lane] = acc[i][j];
-  __threadfence();
+    for (int j = 0; j < NT; j++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), prs, at(slice, i, j), 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ int last;
-  if (threadIdx.x == 0) last = (atomicAdd(&g.counter[tile], 1) == g.slices - 1);
+  if (threadIdx.x == 0) last = splitk_arrive((unsigned *)g.counter + tile, (unsigned)g.slices);
   __syncthreads();
   if (!last) return;
-  __threadfence();
 #pragma unroll
   for (int i = 0; i < MT; i++)
 #pragma unroll
     for (int j = 0; j < NT; j++) {
-      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-      for (int sl = 0; sl < g.slices; sl++) {
-        const f32x4 v = __builtin_nontemporal_load(
-            (const f32x4 *)(g.partial + ((int64_t)sl * tiles + tile) * tile_elems) + (lin0 + (i * NT + j) * 256) / 4 + lane);
+      f32x4 sum = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, at(0, i, j), 0, 16));  // slab 0 as is
+      for (int sl = 1; sl < g.slices; sl++) {
+        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, at(sl, i, j), 0, 16));
         sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
       }
       store(i, j, sum);
     }
-  if (threadIdx.x == 0) g.counter[tile] = 0;
 }
 
 // Direct-load variant (any K % 32 == 0): 4 waves in a WM × WN grid, wave tile MT weight tiles

@@ -9,6 +9,8 @@ These tests build the states directly rather than hoping a test order recreates 
   * counters of every split-K route read zero after every call, results on the oracle;
   * kpart's two K slices into a page-locked host output region (no float atomics there).
 Parity is against the oracle (core/GGMLComputeOps.kt:70-145) at the §8c bar."""
+import re
+
 import numpy as np
 import pytest
 
@@ -171,20 +173,19 @@ def test_concurrent_streams_do_not_share_scratch(gpu, oracle):
     assert G.syncCountersSum() == 0
 
 
-def test_counter_growth_behind_a_busy_null_stream(gpu, oracle):
-    """Round 4's resident-graph failure, built directly: round 4 zeroed newly grown tile
-    counters with hipMemset on the null stream, which the library's non-blocking stream does not wait
-    for. With torch's default (null) stream busy, the GEMM could run on unzeroed (recycled) counter
-    words: on such a tile no slice saw itself last, so its outputs were never written (exact zeros).
-    Host-path calls of the graph test's down-projection shape (gemm_q_*: 12 K slices, a counter per
-    tile), each queued behind ~10 ms of torch work on the default stream, the last one growing the
-    counters past their 4096-tile floor (hipMemsetAsync on the launch stream since round 5)."""
+def test_split_k_behind_a_busy_null_stream(gpu, oracle):
+    """Round 4 zeroed newly grown tile counters with hipMemset on the null stream, which the library's
+    non-blocking stream does not wait for. Host-path calls of the graph test's
+    down-projection shape (gemm_q_*: 12 K slices, a counter per tile, the sc1 hand-off), each queued
+    behind ~10 ms of torch work on the default (null) stream, after recycled device memory was filled
+    with -1: no tile may come back unwritten, every result on the oracle, counters zero after. Since
+    round 5 the counters are zeroed by hipMemsetAsync on the launch stream, at a 4096-tile floor that
+    no split-K grid reaches (split K stops at ~2 workgroups per CU)."""
     import torch
     import ggml_hip as G
     K, N, RB = 384, 4, 384 // 32 * 18
     sq = torch.randn(2048, 2048, device="cuda") / 64
-    grew = False
-    for M in (256, 128 * 40, 128 * 4097 + 64):
+    for M in (256, 128 * 40, 128 * 41 + 64):
         q = oracle.quantize(2, random_weights(M * K, M % 1000))
         x = random_acts(K * N, M % 1000 + 1).reshape(K, N)
         junk = torch.full((1 << 22,), -1, dtype=torch.int32, device="cuda")  # recycled memory is not zero
@@ -194,16 +195,12 @@ def test_counter_growth_behind_a_busy_null_stream(gpu, oracle):
         y = sq
         for _ in range(60):  # the null stream busy; nothing waits for it
             y = y @ sq
-        e0 = G.debugScratchEpoch()
         G.debugRoute()
         got = gpu_matmul(2, q, M, K, N, x, host=True)
         route = G.debugRoute()
-        grew |= G.debugScratchEpoch() > e0
-        assert "gemm_q_" in route, route
+        m = re.search(r"gemm_q_\w+<[^>]*>:t\d+s(\d+)", route)
+        assert m and int(m.group(1)) > 1, route  # split K
         assert not any((got[t:t + 64] == 0).all() for t in range(0, M, 64)), (M, route)  # no unwritten tile
-        rows = np.unique(np.concatenate([np.arange(0, M, 97), [M - 1]]))  # rows of every tile
-        qs = np.ascontiguousarray(q.reshape(M, RB)[rows]).reshape(-1)
-        _check_oracle(oracle, 2, qs, rows.size, K, x, got[rows])
+        _check_oracle(oracle, 2, q, M, K, x, got)
     torch.cuda.synchronize()
-    assert grew, "no call grew the scratch"
     assert G.syncCountersSum() == 0
