@@ -348,7 +348,11 @@ int cu_count() {
 
 template <int QT, int CPL>
 void launch_stream_t(int grid, const GemvDesc &single, const StreamWork *work, int spw, hipStream_t st, const PeerDesc *peer) {
+#ifdef LK_PF
+  constexpr size_t lds = StreamGeom<QT, CPL>::LDS + kStreamWaves * 1024;  // lab: the prefetch landing slots
+#else
   constexpr size_t lds = StreamGeom<QT, CPL>::LDS;
+#endif
   if (peer)
     hipLaunchKernelGGL((gemv_stream_peer_kernel<QT, CPL>), dim3(grid), dim3(kStreamWaves * 64), lds, st, work, spw, peer);
   else
@@ -1653,6 +1657,10 @@ struct lk_plan {
   unsigned *sync = nullptr;  // chain plans: barrier counters, exit counter, timeout flag
   int nbar = 0;
   const PeerDesc *peer = nullptr;  // one rank of a multi-GPU chain (lk_p2p_chain): device PeerDesc
+#ifdef LK_PF
+  const StreamWork *pf_work = nullptr;  // lab: the successor plan's first group (same grid)
+  int pf_spw = 0;
+#endif
 };
 
 namespace {
@@ -1967,8 +1975,16 @@ int lk_sync_counters_sum(uint64_t *sum) {
 int lk_plan_launch(lk_plan *plan, void *stream) {
   if (!plan) return fail(LK_ERR_INVALID_ARG, "null plan");
   hipStream_t st = pick_stream(stream);
-  for (auto &g : plan->groups) {
-    int rc = launch_stream(g.qt, g.cls, g.grid, GemvDesc{}, g.work, g.spw, st, plan->peer);
+  for (size_t k = 0; k < plan->groups.size(); k++) {
+    auto &g = plan->groups[k];
+    GemvDesc pf{};
+#ifdef LK_PF
+    if (k + 1 == plan->groups.size() && plan->pf_work) {  // lab: the last group prefetches for the successor
+      pf.a = (const uint8_t *)plan->pf_work;
+      pf.M = plan->pf_spw;
+    }
+#endif
+    int rc = launch_stream(g.qt, g.cls, g.grid, pf, g.work, g.spw, st, plan->peer);
     if (rc) return rc;
   }
   for (auto &s : plan->singles) {
@@ -1977,6 +1993,22 @@ int lk_plan_launch(lk_plan *plan, void *stream) {
   }
   return LK_OK;
 }
+
+#ifdef LK_PF
+// lab only (not in include/lk_hip.h): plan's last launch prefetches `next`'s first units per wave;
+// `next` must outlive every launch of `plan`. NULL unlinks.
+extern "C" int lk_plan_prefetch_next(lk_plan *plan, const lk_plan *next) {
+  if (!plan) return fail(LK_ERR_INVALID_ARG, "null plan");
+  plan->pf_work = nullptr;
+  plan->pf_spw = 0;
+  if (!next || plan->sync || next->sync || plan->groups.empty() || next->groups.empty()) return LK_OK;
+  const auto &a = plan->groups.back(), &b = next->groups.front();
+  if (a.grid != b.grid || a.qt != b.qt) return LK_OK;  // same grid and block type only
+  plan->pf_work = b.work;
+  plan->pf_spw = b.spw;
+  return LK_OK;
+}
+#endif
 
 int lk_plan_num_launches(const lk_plan *plan) {
   return plan ? (int)(plan->groups.size() + plan->singles.size()) : 0;

@@ -490,6 +490,32 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
     const unsigned ep = __hip_atomic_load(peer->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     cross_target = (unsigned)peer->P * (ep + 1u);
   }
+#ifdef LK_PF
+  // lab (decode-chain prefetch): a plan launch may carry its successor plan's work list in s_a (its
+  // slots per workgroup in s_M, the same grid): each wave first reads the first LK_PF units of its
+  // rows there with default-policy LDS-DMA into a landing slot of its own that nobody reads (past
+  // the kernel's LDS), so they are in L2 / the Infinity Cache when the successor starts. Issued
+  // before everything else, so the counted vmcnt waits below (youngest-first) still hold.
+  if (wk && s_a && !PEER) {
+    const StreamWork *nw = (const StreamWork *)s_a + (int64_t)blockIdx.x * s_M;
+    const __attribute__((address_space(4))) StreamWork *cw = (const __attribute__((address_space(4))) StreamWork *)nw;
+    const uint8_t *na = cw->a;
+    const int nK = cw->K, nrb = cw->row_begin, nre = cw->row_end;
+    if (cw->sync == nullptr) {
+      const int nNP = nK >> 6, nnch = (nNP + 63) >> 6;
+      const int64_t nRB = (int64_t)nNP * G::PB;
+      const int nper = (nre - nrb + kStreamWaves - 1) / kStreamWaves;
+      const int nr0 = min(nrb + wave * nper, nre), nrows = min(nr0 + nper, nre) - nr0;
+      const int64_t bytes = min((int64_t)LK_PF * G::UB, (int64_t)nrows * nnch * G::UB);  // rows are contiguous
+      const LK_GLOBAL uint8_t *base = (const LK_GLOBAL uint8_t *)na + (int64_t)nr0 * nRB;
+      LK_LDS uint8_t *land = (LK_LDS uint8_t *)((uint8_t *)lds + G::LDS + wave * 1024);
+      for (int64_t o = 0; o < bytes; o += 1024) {
+        const int64_t off = o + lane * 16 < bytes ? o + lane * 16 : 0;
+        __builtin_amdgcn_global_load_lds((const LK_GLOBAL void *)(base + off), (LK_LDS void *)land, 16, 0, 0);
+      }
+    }
+  }
+#endif
   for (int si = 0; si < nseg; si++) {
     const uint8_t *a_node;
     const float *x_node;
