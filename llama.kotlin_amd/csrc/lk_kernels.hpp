@@ -2275,8 +2275,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
 // Every wave issues the same DMA count per stage (CW), so a counted vmcnt plus one barrier
 // publishes a stage. Q4_0 codes carry their -8 offset ((n - 8)·2^-9, exact), so no T input.
 // Split K: each slice stores an f32 partial slab; splitk_reduce_kernel sums them in order.
+// LK_WIDE_SCHED bit 1 (the product since round 5): the scale FMAs interleaved with the MFMAs by
+// sched_group_barrier (C5 57.8-58.6 -> 56.6-57.4 us per call, A/B three rounds on one box); bit 0
+// (lab): scalar instead of packed scale FMAs (58.6-59.4 -> 60.0-61.0 us: slower)
 #ifndef LK_WIDE_SCHED
-#define LK_WIDE_SCHED 0  // lab builds: bit 0 scalar scale FMAs, bit 1 MFMA/VALU interleave (sched_group_barrier)
+#define LK_WIDE_SCHED 2
 #endif
 template <int QT> struct WideGeom {
   static constexpr int NW = 8, KG = 2, MW = NW / KG;             // waves: MW along M x KG K-groups
