@@ -628,8 +628,10 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
 #pragma unroll
       for (int k = 0; k < G::D; k++) {
         const bool real = k < nunits;
+        // a filler (past the wave's last unit) has every lane read the node's first 16 bytes: one
+        // cache line per instruction for the CU's address path instead of sixteen (never decoded)
         const LK_GLOBAL uint8_t *base = real ? A + (int64_t)irow * RB + (int64_t)ich * G::UB : (const LK_GLOBAL uint8_t *)a_node;
-        const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : (int)min((int64_t)G::UB, RB);
+        const int ubytes = real ? (int)min((int64_t)G::UB, RB - (int64_t)ich * G::UB) : 16;
         dma_unit(base, ubytes, k);
         if (real) {
           advance();
