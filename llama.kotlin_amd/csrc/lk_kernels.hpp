@@ -265,6 +265,7 @@ __global__ __launch_bounds__(256) void gemv_q_n1_kernel(const GemvDesc d) {
 // Q8 decode: bytes biased to unsigned (xor 0x80) go through v_cvt_f32_ubyteN.
 
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 #define LK_LDS __attribute__((address_space(3)))
 
 // The weight stream's LDS-DMA uses cache policy nt (aux 2: bytes read once per launch). The
@@ -2117,21 +2118,19 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     uint32_t hi[4], lo[4];
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {
-      uint32_t hh[2], ll[2];
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const uint32_t bx = __builtin_bit_cast(uint32_t, v[i][e + q]);
-        const float r = v[i][e + q] - __builtin_bit_cast(float, bx & 0xFFFF0000u);  // exact
-        uint32_t br = __builtin_bit_cast(uint32_t, r);
-        br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even
-        hh[q] = bx;
-        ll[q] = br;
-        // Q4_0's −136·Σx cancels against Σ (128 + n)·(hi + lo): sum the split itself, so the
-        // split's own error is not amplified
-        hsum += __builtin_bit_cast(float, bx & 0xFFFF0000u) + __builtin_bit_cast(float, br & 0xFFFF0000u);
-      }
-      hi[e / 2] = __builtin_amdgcn_perm(hh[1], hh[0], 0x07060302u);
-      lo[e / 2] = __builtin_amdgcn_perm(ll[1], ll[0], 0x07060302u);
+      // hi = x truncated to bf16, lo = x − hi (exact in f32) rounded to nearest even by one
+      // v_cvt_pk_bf16_f32 for the pair (round 5: the same bits as the former per-element integer
+      // rounding, about half the VALU of the split)
+      const uint32_t b0 = __builtin_bit_cast(uint32_t, v[i][e]), b1 = __builtin_bit_cast(uint32_t, v[i][e + 1]);
+      const float h0 = __builtin_bit_cast(float, b0 & 0xFFFF0000u), h1 = __builtin_bit_cast(float, b1 & 0xFFFF0000u);
+      const f2v r = {v[i][e] - h0, v[i][e + 1] - h1};  // exact
+      const uint32_t lp = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
+      hi[e / 2] = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
+      lo[e / 2] = lp;
+      // Q4_0's −136·Σx cancels against Σ (128 + n)·(hi + lo): sum the split itself, so the
+      // split's own error is not amplified
+      hsum += h0 + __builtin_bit_cast(float, lp << 16);
+      hsum += h1 + __builtin_bit_cast(float, lp & 0xFFFF0000u);
     }
     u32x4 *xf = (u32x4 *)(xlds + (f * kXSplits) * 1024) + lane;
     xf[0] = u32x4{hi[0], hi[1], hi[2], hi[3]};
@@ -2143,11 +2142,14 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       if (lane < 16) tlds[f * 16 + lane] = QT == LK_TYPE_Q4_0 ? -136.f * part : part;
     }
   }
+  [[maybe_unused]] const uint64_t t_split = LK_KP_T();  // (lab stamps) activations in, split, in LDS
   // 2. the weight ring, after the split
   if (myL)
     for (int u = 0; u < min(D, nunits); u++) issue(u, u);
   wait_lgkmcnt0();
+  [[maybe_unused]] const uint64_t t_issued = LK_KP_T();
   __builtin_amdgcn_s_barrier();  // fragments and flags visible (bare: the ring stays in flight)
+  [[maybe_unused]] const uint64_t t_bar = LK_KP_T();
   // 3. this wave holds the fragments of its 8 blocks
   u32x4 xh[8][NT], xl[8][NT];
 #pragma unroll
@@ -2190,6 +2192,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       // ops younger than this unit's DMA: its successors already issued, and the stores since
       wait_vmcnt_rt<G::MAXW>(myL * min(D - 1, nunits - 1 - u) + min(u, D) * SH);
       asm volatile("" ::: "memory");
+#ifdef LK_LAB_STAMPS
+      if (u == 0) LK_KP_SET(9, LK_KP_T());  // the first unit has landed
+#endif
       uint32_t wd[8][G::WPB];
       const uint8_t *slot_ptr = ring + slot * G::SLOT;
       {
@@ -2257,7 +2262,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
                            g.d_nb0, g.d_nb1, lane);
   }
   LK_KP_SET(0, t_entry); LK_KP_SET(2, t_loop); LK_KP_SET(3, t_end); LK_KP_SET(4, LK_KP_T());
-  LK_KP_SET(8, (uint64_t)nunits);
+  LK_KP_SET(8, (uint64_t)nunits); LK_KP_SET(1, t_split); LK_KP_SET(5, t_issued); LK_KP_SET(6, t_bar);
 }
 
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------
