@@ -1669,6 +1669,35 @@ namespace {
 // balanced by weight bytes, cut at node boundaries into segments.
 void split_rows(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<std::vector<StreamWork>> &per);
 
+// Adjacent nodes that read the same activations and whose weight rows and output rows continue each
+// other in memory (a model's q, k and v projections allocated back to back; gate and up) become one
+// node, so the launch's rows split evenly over its waves: per-node workgroup shares gave the q, k, v
+// stage 48 or 49 rows per workgroup (85.3 workgroups per node), and the 49-row workgroups' waves ran a
+// seventh row and ended the launch ~0.8 µs late (lab stamps). Same bits either way:
+// every row is one wave's dot. LK_NO_MERGE=1 keeps the nodes apart (A/B).
+void merge_adjacent(std::vector<GemvDesc> &descs, int32_t qt) {
+  static const bool off = [] {
+    const char *e = std::getenv("LK_NO_MERGE");
+    return e && *e == '1';
+  }();
+  if (off || descs.size() < 2) return;
+  const int64_t pb = stream_pair_bytes(qt);
+  std::vector<GemvDesc> out;
+  for (const GemvDesc &d : descs) {
+    if (!out.empty()) {
+      GemvDesc &p = out.back();
+      const int64_t row_bytes = (int64_t)(p.K / 64) * pb;
+      if (p.x == d.x && p.K == d.K && p.dst_row_stride == d.dst_row_stride && d.a == p.a + (int64_t)p.M * row_bytes &&
+          d.dst == p.dst + (int64_t)p.M * p.dst_row_stride && (int64_t)p.M + d.M <= INT32_MAX) {
+        p.M += d.M;
+        continue;
+      }
+    }
+    out.push_back(d);
+  }
+  descs.swap(out);
+}
+
 void build_work(const std::vector<GemvDesc> &descs, int32_t qt, int grid, std::vector<StreamWork> &work, int *spw) {
   std::vector<std::vector<StreamWork>> per;
   split_rows(descs, qt, grid, per);
@@ -1809,6 +1838,7 @@ int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
     const int32_t qt = kv.first;
     const int cls = type_cls[qt];
     auto &descs = kv.second;
+    merge_adjacent(descs, qt);
     int64_t rows = 0;
     for (auto &d : descs) rows += d.M;
     const int grid = stream_grid(rows);
@@ -1876,6 +1906,7 @@ int lk_detail_chain_create(const lk_tensor *a, const lk_tensor *b, const lk_tens
   std::vector<std::vector<StreamWork>> per(grid);
   for (size_t s = 0; s < stages.size(); s++) {
     std::vector<std::vector<StreamWork>> ps;
+    merge_adjacent(stages[s], qt);
     split_rows(stages[s], qt, grid, ps);
     for (int g = 0; g < grid; g++) {
       if (ps[g].empty()) {  // no rows here: the workgroup still takes part in the barrier

@@ -69,7 +69,11 @@ def main():
             by = {x: {"entry_med": round(float(np.median([entry[w] for w in wgs if w % 8 == x])), 2),
                       "exit_med": round(float(np.median([exit_[w] for w in wgs if w % 8 == x])), 2)} for x in range(8)}
             ex = np.array(list(exit_.values()))
-            reps.append({"exit_med": round(float(np.median(ex)), 2), "exit_max": round(float(ex.max()), 2), "by_xcd": by})
+            units = {w: int(st[w, live[w], 8].sum()) for w in wgs}
+            late = sorted(wgs, key=lambda w: -exit_[w])[:8]
+            reps.append({"exit_med": round(float(np.median(ex)), 2), "exit_max": round(float(ex.max()), 2), "by_xcd": by,
+                         "latest": [[int(w), round(float(exit_[w]), 2), round(float(entry[w]), 2), units[w]] for w in late],
+                         "units_med": int(np.median(list(units.values())))})
         out["b2b_" + "+".join(bench.CHAIN[last])] = reps
     for p in chain:
         p.close()
