@@ -129,3 +129,53 @@ def test_chain_rejects_what_it_cannot_stream(gpu):
     d2 = G.GGMLTensor(G.GGMLType.F32, [2, 512], bufferId=ga.addBuffer(8 * 512))
     with pytest.raises(NotImplementedError):
         G.MulMatPlan(ga, [(a, b2, d2)], stages=[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("qt", [2, 3, 12])
+def test_plan_fuses_adjacent_nodes_bit_exactly(gpu, qt):
+    """lk_plan_create fuses adjacent nodes that read the same activations and whose weight rows and
+    output rows continue each other in memory (a model's q, k, v back to back: one even row split).
+    Three such nodes in one weight buffer and one output buffer, plus a fourth whose weights sit
+    after a gap (not fused), as a plan and as a chain stage: every output bit-equal to the nodes
+    launched one by one; and the fused form equal to the same plan with the nodes apart (LK_NO_MERGE
+    is read once per process, so the comparison is against single launches)."""
+    import ggml_hip as G
+    K, Ms = 1024, (512, 256, 768, 512)
+    bb = {2: 18, 3: 20, 12: 144}[qt]
+    per = 256 if qt == 12 else 32
+    row = K // per * bb
+    ga = G.GGMLGraphAllocator(device="cuda", defaultBufferSize=16)
+    wbuf = ga.addBuffer(sum(Ms) * row + 4096 + 256)
+    obuf = ga.addBuffer(4 * sum(Ms) + 256)
+    xb = ga.addBuffer(4 * K + 64)
+    x = G.GGMLTensor(G.GGMLType.F32, [1, K], bufferId=xb)
+    ga.setTensorBytes(x, random_acts(K, 7).view(np.uint8))
+    nodes, woff, ooff = [], 0, 0
+    for i, M in enumerate(Ms):
+        if i == 3:
+            woff += 4096  # a gap: not contiguous with the node before
+        if qt == 12:
+            q = np.random.default_rng(40 + i).integers(0, 256, M * K // 256 * 144, dtype=np.uint8)
+            q.reshape(-1, 144)[:, 0:4] = np.frombuffer(np.array([0.01, 0.001], np.float16).tobytes(), np.uint8)
+        else:
+            q = O.quantize(qt, random_weights(M * K, 40 + i, std=1.0 / np.sqrt(K)))
+        a = G.GGMLTensor(G.GGMLType(qt), [K, M], bufferId=wbuf, dataOffset=woff)
+        ga.setTensorBytes(a, q)
+        d = G.GGMLTensor(G.GGMLType.F32, [1, M], bufferId=obuf, dataOffset=ooff)
+        nodes.append((a, x, d))
+        woff += M * row
+        ooff += 4 * M
+    want = []
+    for (a, b, d) in nodes:
+        G.computeMatMul(ga, None, a, b, d)
+        want.append(bytes(ga.tensorBytes(d)))
+    for form in ("plan", "chain"):
+        ga.setTensorBytes(G.GGMLTensor(G.GGMLType.F32, [1, sum(Ms)], bufferId=obuf), np.zeros(4 * sum(Ms), np.uint8))
+        p = G.MulMatPlan(ga, nodes) if form == "plan" else G.MulMatPlan(ga, nodes, stages=[0] * len(nodes))
+        p.launch()
+        import torch
+        torch.cuda.synchronize()
+        got = [bytes(ga.tensorBytes(d)) for (_, _, d) in nodes]
+        assert got == want, form
+        p.close()
