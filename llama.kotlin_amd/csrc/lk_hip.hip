@@ -40,10 +40,12 @@ void note_route(const char *fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  if (g_route.size() < 4096) {
-    if (!g_route.empty()) g_route += ' ';
-    g_route += buf;
+  if (g_route.size() >= 4096) {  // bounded: keep the newest words (a caller that never clears)
+    const size_t cut = g_route.find(' ', g_route.size() / 2);
+    g_route.erase(0, cut == std::string::npos ? g_route.size() : cut + 1);
   }
+  if (!g_route.empty()) g_route += ' ';
+  g_route += buf;
 }
 
 int fail(int st, const char *fmt, ...) {
