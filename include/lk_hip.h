@@ -223,7 +223,7 @@ const char *lk_debug_route(void);
 void lk_debug_route_clear(void);
 /* Diagnostic: how many times the batched kernels' device scratch (activation fragments, split-K
  * slabs, tile counters) of the current device was reallocated. Outgrown buffers are retired, never
- * freed before lk_shutdown, so HIP graphs captured earlier stay valid (INTEGRATION.md §3c). */
+ * freed before lk_shutdown, so HIP graphs captured earlier stay valid (INTEGRATION.md §5a). */
 uint64_t lk_debug_scratch_epoch(void);
 
 /* ---- multi-GPU: row shards + RCCL all-gather over xGMI -----------------
