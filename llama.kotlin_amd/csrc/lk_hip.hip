@@ -2784,3 +2784,12 @@ extern "C" int lk_lab_stamps_clear(void) {
   return hipMemcpyToSymbol(HIP_SYMBOL(lk::lk_kp_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : 5;
 }
 #endif
+#ifdef LK_LAB_CHAIN_STAMPS
+extern "C" int lk_lab_chain_stamps(uint64_t *out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(lk::lk_chain_stamps), sizeof(uint64_t) * (size_t)std::min(n, 256 * 256 * 8)) == hipSuccess ? 0 : 5;
+}
+extern "C" int lk_lab_chain_stamps_clear(void) {
+  static uint64_t zero[256 * 256 * 8];
+  return hipMemcpyToSymbol(HIP_SYMBOL(lk::lk_chain_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : 5;
+}
+#endif

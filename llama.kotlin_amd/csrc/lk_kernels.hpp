@@ -291,6 +291,15 @@ __device__ uint64_t lk_kp_stamps[1024][8][10];
 #define LK_KP_T() 0ull
 #define LK_KP_SET(i, v) do { } while (0)
 #endif
+// Lab (-DLK_LAB_CHAIN_STAMPS, never the product): per (workgroup, segment) stamps of the stream
+// kernel's wave 0, lane 0 — slot 0 segment start, 1 stores drained (grid barrier), 2 released, 3
+// image ready, 4 x in VGPRs, 5 first unit landed, 6 segment done, 7 the segment's barrier number
+#ifdef LK_LAB_CHAIN_STAMPS
+__device__ uint64_t lk_chain_stamps[256][256][8];
+#define LK_CS(i, v) do { if (tid == 0 && blockIdx.x < 256 && si < 256) lk_chain_stamps[blockIdx.x][si][i] = (v); } while (0)
+#else
+#define LK_CS(i, v) do { } while (0)
+#endif
 
 struct StreamWork {
   const uint8_t *a;
@@ -550,6 +559,7 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
     const int nrows = __builtin_amdgcn_readfirstlane(min(r0 + per_w, re) - r0);
     const int nunits = nrows * nch;
     st_units += nunits;
+    LK_CS(0, __builtin_amdgcn_s_memrealtime()); LK_CS(7, (uint64_t)bar);
 #ifdef LK_LAB_STAMPS
     asm volatile("" ::"s"(nunits));
     if (si == 0) t_rec = LK_KP_T();
@@ -650,6 +660,7 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
       //    one 128-B line each); the shard's last arriver arrives on the top word
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      LK_CS(1, __builtin_amdgcn_s_memrealtime());
       unsigned *bsync = sync + (bar - 1) * kChainLine * 9;
       if (wave == 0 && lane == 0) {
         const int sh = (int)blockIdx.x % 8;
@@ -685,6 +696,7 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
           __builtin_amdgcn_s_sleep(2);
         }
       }
+      LK_CS(2, __builtin_amdgcn_s_memrealtime());
       asm volatile("" ::: "memory");  // the loads below stay after the poll
       __builtin_amdgcn_s_barrier();
       // 4. the stage's activations (sc1 loads: the youngest, so wait for all)
@@ -721,6 +733,7 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
     if (si == 0) t_img = LK_KP_T();
 #endif
     }
+    LK_CS(3, __builtin_amdgcn_s_memrealtime());
 
     // 2. activations into VGPRs in decode order, and Σx per block (only the node's own chunks:
     //    a grouped launch runs every node at its largest node's class; A/B, four rounds: layer
@@ -779,6 +792,10 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
     asm volatile("" ::"v"(xs0[0]), "v"(xs1[0]));
     if (si == 0) t_x = LK_KP_T();
 #endif
+#ifdef LK_LAB_CHAIN_STAMPS
+    asm volatile("" ::"v"(xs0[0]), "v"(xs1[0]));
+    LK_CS(4, __builtin_amdgcn_s_memrealtime());
+#endif
     int slot = 0, u = 0;
     LK_GLOBAL float *out = (LK_GLOBAL float *)dst_node + (int64_t)r0 * dst_stride;
     for (int row = 0; row < nrows; row++) {
@@ -797,6 +814,7 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
 #ifdef LK_LAB_STAMPS
           if (si == 0 && u == 0) t_u0 = LK_KP_T();
 #endif
+          if (u == 0) LK_CS(5, __builtin_amdgcn_s_memrealtime());
           const uint32_t *rp = (const uint32_t *)(ring + slot * G::SLOT + lane * G::PB);
           uint32_t w[G::PDW];
           u32x4 kh, kc0, kc1;  // Q4_K: block lane/4's header and sub-blocks 2(lane%4), +1
@@ -840,6 +858,7 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
+    LK_CS(6, __builtin_amdgcn_s_memrealtime());
   }
   LK_KP_SET(0, t_entry); LK_KP_SET(4, LK_KP_T()); LK_KP_SET(8, (uint64_t)st_units);
   LK_KP_SET(1, t_rec); LK_KP_SET(2, t_iss); LK_KP_SET(3, t_img); LK_KP_SET(5, t_x); LK_KP_SET(6, t_u0);
