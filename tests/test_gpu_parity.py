@@ -390,6 +390,8 @@ WIDE = [
     (257, 1024, 100),   # ragged columns (a 4-column x-tile) and a 1-row tail
     (64, 11008, 48),    # one row tile, long K
     (1024, 512, 33),    # the smallest wide N
+    (128, 4096, 80),    # in-launch split (N % 16 == 0): a column tile with one real x-tile
+    (512, 2048, 160),   # in-launch split, three column tiles
 ]
 
 

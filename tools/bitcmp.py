@@ -8,7 +8,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "llama.kotlin_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
 
 CASES = [(2, 11008, 4096, 32), (3, 11008, 4096, 32), (2, 4096, 11008, 32), (2, 11008, 4096, 24), (2, 4096, 4096, 512),
-         (2, 11008, 4096, 16), (3, 4096, 4096, 8), (6, 4096, 4096, 32)]
+         (2, 11008, 4096, 16), (3, 4096, 4096, 8), (6, 4096, 4096, 32),
+         (3, 4096, 4096, 512), (2, 4096, 11008, 64), (3, 2048, 4096, 48), (2, 1024, 4096, 80), (6, 1024, 4096, 96)]
 
 
 def main():
