@@ -71,8 +71,15 @@ def main():
             ex = np.array(list(exit_.values()))
             units = {w: int(st[w, live[w], 8].sum()) for w in wgs}
             late = sorted(wgs, key=lambda w: -exit_[w])[:8]
+            # within a workgroup: its last wave's exit against its waves' mean and earliest exit
+            wex = {w: (st[w, live[w], 4] - t0) / 100 for w in wgs}
+            intra = np.array([wex[w].max() - wex[w].mean() for w in wgs])
+            intra_first = np.array([wex[w].max() - wex[w].min() for w in wgs])
             reps.append({"exit_med": round(float(np.median(ex)), 2), "exit_max": round(float(ex.max()), 2), "by_xcd": by,
                          "latest": [[int(w), round(float(exit_[w]), 2), round(float(entry[w]), 2), units[w]] for w in late],
+                         "intra_wg_last_minus_mean_med": round(float(np.median(intra)), 2),
+                         "intra_wg_last_minus_first_med": round(float(np.median(intra_first)), 2),
+                         "latest_wg_last_minus_mean": [round(float(wex[w].max() - wex[w].mean()), 2) for w in late],
                          "units_med": int(np.median(list(units.values())))})
         out["b2b_" + "+".join(bench.CHAIN[last])] = reps
     for p in chain:
