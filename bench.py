@@ -134,6 +134,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-multi-gpu-cost", action="store_true")
+    ap.add_argument("--no-throughput", action="store_true", help="skip the multi_gpu_throughput legs")
     ap.add_argument("--cpu-sample-rows", type=int, default=6144)
     ap.add_argument("--sharded", action="store_true",
                     help="the N > 1 path (C-ABI RCCL communicator + lk_sharded_plan) at any world size")
@@ -324,8 +325,13 @@ def main():
         "metric": "Q4_0 matmul GB/s + tokens/sec 7B, 1/2/4/8 MI355X vs Kotlin CPU",
         "value": round(value_gbs, 2),
         "unit": "GB/s",
-        # tokens/s of the dependent decode order (decode_chain); the timed grouped step's own rate beside it
-        "tokens_per_s": decode.get("tokens_per_s") if isinstance(decode, dict) else None,
+        # tokens/s of the dependent decode order (decode_chain); the timed grouped step's own rate beside it.
+        # Never null: without a decode figure (--no-chain, or the section failed) it falls back
+        # to the grouped step's rate, and tokens_per_s_source names which one it is
+        "tokens_per_s": (decode["tokens_per_s"] if isinstance(decode, dict) and decode.get("tokens_per_s")
+                         else round(tokens / elapsed, 2)),
+        "tokens_per_s_source": ("decode_chain" if isinstance(decode, dict) and decode.get("tokens_per_s")
+                                else "grouped_step"),
         "tokens_per_s_grouped_step": round(tokens / elapsed, 2),
         "n_gpus": world,
         "steps": args.steps,
@@ -371,6 +377,14 @@ def main():
         section("persistent_chain", lambda: {
             "layer_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 1),
             "decode_stages": persistent_chain(torch, G, ga, nodes_by_layer, compute, token_bytes, 4)})
+    if not args.no_throughput and (comm is not None or world == 1):
+        # every rank takes part (the legs' sharded plans gather over the world); world 1 without
+        # --sharded uses a one-rank communicator: the same code path
+        tcomm = comm if comm is not None else G.Comm.single()
+        section("multi_gpu_throughput", lambda: multi_gpu_throughput(torch, G, dev, tcomm, world, rank,
+                                                                      dist if distributed else None))
+        if comm is None:
+            tcomm.close()
     if rank == 0 and world == 1 and not args.no_headline:
         section("headline_q4_0_4096x4096_n1", lambda: headline(torch, G, dev))
     if rank == 0 and world == 1 and not args.no_batched:
@@ -582,6 +596,172 @@ def multi_gpu_world1(torch, G, ga, nodes_by_layer, stream, reps=5):
     for p in p2p + rccl:
         p.close()
     group.close(); comm.close()
+    return out
+
+
+# ---- the north star's "4096x4096xbatch throughput at 1/2/4/8 GPUs"  ----------------
+# Every leg is a set of independent MUL_MAT calls on distinct weights, each call row-sharded over the
+# world through lk_sharded_plan (local rows + one RCCL group of in-place all-gathers, the exact code the
+# decode path uses), at every world size — world 1 included (a one-rank communicator). Total work per
+# call is fixed, so the driver's 1 -> 8 runs read a strong-scaling curve per leg.
+THROUGHPUT_LEGS = [
+    # (name, node shapes (M, K) of one call, batch N)
+    ("q4_0_4096x4096_n1", [(4096, 4096)], 1),
+    ("q4_0_4096x4096_n32", [(4096, 4096)], 32),
+    ("q4_0_4096x4096_n512", [(4096, 4096)], 512),
+    ("llama7b_layer_q4_0_n32", [(M, K) for (_, M, K) in LAYER_MATS], 32),
+]
+MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (MI355X_MICROARCH.md); the batched kernels run bf16 hi/lo MFMAs
+
+
+def leg_geometry(shapes, N, world, min_rank_bytes=300e6):
+    """Per-call quantities of a throughput leg at `world` ranks and how many distinct weight copies a
+    timed pass rotates over, so that each rank streams >= min_rank_bytes of distinct weights per pass
+    (more than the 256 MiB Infinity Cache at every world size: the weights come from HBM)."""
+    for (M, _) in shapes:
+        if M % world:
+            raise ValueError(f"M = {M} does not split over {world} ranks")
+    w_full = sum(M * K // 32 * Q4_0_BLOCK for (M, K) in shapes)
+    copies = max(2, -(-int(min_rank_bytes) // max(1, w_full // world)))
+    out_bytes = sum(4 * N * M for (M, _) in shapes)
+    return {"copies": copies,
+            "alg_bytes_per_call": sum(alg_bytes(M, K, N) for (M, K) in shapes),
+            "useful_flop_per_call": sum(2 * M * N * K for (M, K) in shapes),
+            "rank_alg_bytes_per_call": sum(alg_bytes(M // world, K, N) for (M, K) in shapes),
+            "rank_flop_per_call": sum(2 * (M // world) * N * K for (M, K) in shapes),
+            "gather_bytes_in_per_rank": out_bytes * (world - 1) // world,
+            "output_bytes_per_call": out_bytes}
+
+
+def throughput_leg(torch, G, dev, comm, world, rank, dist, name, shapes, N, reps=5, keep=None, min_rank_bytes=300e6):
+    """One leg: `copies` calls of `shapes` at batch N (synthetic Q4_0 weights: every rank quantizes the
+    same full matrices and keeps its row shard, so the gathered outputs are the single-GPU results),
+    timed three ways on every rank, max over ranks:
+      local     the rank's rows only (its lk_plan per call): per-rank kernel time and roofline;
+      serial    lk_sharded_plan_launch per call: rows, then the RCCL group, one stream;
+      overlap   lk_sharded_plan_launch_split per call: the gathers on a second stream, so call i's
+                exchange overlaps call i+1's rows (the throughput schedule).
+    Check (no oracle in bench.py): rank 0's gathered output of the first call against float64 dot
+    products of dequantizeTensor's weights (bit-exact with the reference, tests/test_gpu_parity.py) on
+    rows sampled from every rank's shard, and the same output's checksum equal on every rank."""
+    T = G.GGMLType
+    geo = leg_geometry(shapes, N, world, min_rank_bytes)
+    copies = geo["copies"]
+    K0 = shapes[0][1]
+    ga = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0xC0FFEE)  # the same full matrices and activations on every rank
+    xs = {K: ga.addBuffer(4 * K * N + 256) for K in {k for (_, k) in shapes}}
+    for K, xb in xs.items():
+        ga.buffers[xb][: 4 * K * N].copy_(torch.randn(K * N, generator=gen, device=dev).view(torch.uint8))
+    shard_q, full_q = [], []
+    for (M, K) in shapes:
+        q = G.quantizeTensor(torch.randn(M * K, generator=gen, device=dev) * 0.02, T.Q4_0)
+        rb = K // 32 * Q4_0_BLOCK
+        per = M // world
+        full_q.append(q if len(full_q) == 0 else None)  # only the first node is checked
+        shard_q.append(q[rank * per * rb:(rank + 1) * per * rb].clone())
+    pitch = [(b.numel() + 255) // 256 * 256 for b in shard_q]
+    wb = ga.addBuffer(copies * sum(pitch) + 256)
+    db = ga.addBuffer(copies * geo["output_bytes_per_call"] + 256 * copies * len(shapes) + 256)
+    sharded, local, dsts, woff, doff = [], [], [], 0, 0
+    for c in range(copies):
+        nodes = []
+        for i, (M, K) in enumerate(shapes):
+            ga.buffers[wb][woff:woff + shard_q[i].numel()].copy_(shard_q[i])
+            a = G.GGMLTensor(T.Q4_0, [K, M // world], bufferId=wb, dataOffset=woff)
+            d = G.GGMLTensor(T.F32, [N, M], bufferId=db, dataOffset=doff)
+            nodes.append((a, G.GGMLTensor(T.F32, [N, K], bufferId=xs[K]), d))
+            woff += pitch[i]
+            doff += (4 * N * M + 255) // 256 * 256
+        sharded.append(G.ShardedMulMatPlan(comm, ga, nodes))
+        local.append(G.MulMatPlan(ga, [(a, b, G.shard_view(d, world, rank)) for (a, b, d) in nodes]))
+        dsts.append([d for (_, _, d) in nodes])
+    del shard_q
+    compute, gather = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+
+    def run_local():
+        for p in local:
+            p.launch(stream=compute)
+
+    def run_serial():
+        for p in sharded:
+            p.launch(stream=compute)
+
+    def run_overlap():
+        for p in sharded:
+            p.launchSplit(compute, gather)
+        compute.wait_stream(gather)
+
+    out = {"N": N, "nodes_per_call": len(shapes), "shapes": [list(s) for s in shapes], "weights": "Q4_0", **geo,
+           "ranks_seen_by_rccl": comm.rcclRanks}
+    for key, fn in (("local", run_local), ("serial", run_serial), ("overlap", run_overlap)):
+        per, graphed = _graph_time(torch, fn, compute, reps)
+        if dist is not None:
+            t = torch.tensor([per], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            per = float(t.item())
+        per /= copies
+        if key == "local":
+            r = {"us_per_call": round(per * 1e6, 3), "rank_GBps": round(geo["rank_alg_bytes_per_call"] / per / 1e9, 1),
+                 "rank_frac_hbm": round(geo["rank_alg_bytes_per_call"] / per / 1e9 / HBM_PEAK_GBS, 4)}
+            if N > 1:
+                r["rank_useful_TFLOPs"] = round(geo["rank_flop_per_call"] / per / 1e12, 2)
+                r["rank_frac_mfma_bf16"] = round(2 * geo["rank_flop_per_call"] / per / 1e12 / MFMA_PEAK_TFS, 4)  # hi + lo
+        else:
+            r = {"us_per_call": round(per * 1e6, 3), "GBps": round(geo["alg_bytes_per_call"] / per / 1e9, 1),
+                 "calls_per_s": round(1 / per, 1)}
+            if N > 1:
+                r["useful_TFLOPs"] = round(geo["useful_flop_per_call"] / per / 1e12, 2)
+        r["hip_graph"] = graphed
+        out[key] = r
+    best = min(out["serial"]["us_per_call"], out["overlap"]["us_per_call"])
+    out["value_GBps"] = round(geo["alg_bytes_per_call"] / (best * 1e-6) / 1e9, 1)
+    if N > 1:
+        out["value_useful_TFLOPs"] = round(geo["useful_flop_per_call"] / (best * 1e-6) / 1e12, 2)
+    # check: the first call's first node, gathered, on every rank
+    torch.cuda.synchronize()
+    M, K = shapes[0]
+    d0 = dsts[0][0]
+    got = ga.buffers[db][d0.dataOffset:d0.dataOffset + 4 * N * M].view(torch.float32).view(M, N)
+    csum = torch.tensor([float(got.double().sum())], dtype=torch.float64, device=dev)
+    same = True
+    if dist is not None:
+        lo, hi = csum.clone(), csum.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        same = bool(lo.item() == hi.item())
+    rows = sorted({int(v) for v in torch.linspace(0, M - 1, 64).tolist()})
+    wq = G.GGMLGraphAllocator(device=str(dev), defaultBufferSize=16)
+    qb = wq.addBuffer(full_q[0].numel() + 256)
+    wq.buffers[qb][: full_q[0].numel()].copy_(full_q[0])
+    wf = G.dequantizeTensor(wq, G.GGMLTensor(T.Q4_0, [K, M], bufferId=qb)).view(M, K)[rows].double()
+    xk = ga.buffers[xs[K]][: 4 * K * N].view(torch.float32).view(K, N).double()
+    ref = wf @ xk
+    err = (got[rows].double() - ref).abs()
+    scale = ref.abs().max().clamp_min(1e-30)
+    rel = float((err / torch.maximum(ref.abs(), 1e-3 * scale)).max())
+    if keep is not None:  # tests: the first call's operands and gathered output, on the host
+        keep.update(q=full_q[0].cpu().numpy(), x=xk.float().cpu().numpy(), got=got.cpu().numpy().copy(), M=M, K=K)
+    out["check"] = {"rows_checked": len(rows), "max_rel_err": rel, "bar": 1e-3, "ok": bool(rel <= 1e-3) and same,
+                    "checksum_equal_on_every_rank": same,
+                    "against": "float64 dot products of dequantizeTensor's weights, rows sampled from every shard"}
+    for p in sharded + local:
+        p.close()
+    del ga, wq
+    return out
+
+
+def multi_gpu_throughput(torch, G, dev, comm, world, rank, dist, legs=None):
+    """Every THROUGHPUT_LEGS leg at this world size (see throughput_leg)."""
+    out = {"world": world, "scaling": "strong (total work per call fixed; ranks split every matrix's rows)",
+           "exchange": "in-place RCCL all-gather of each call's outputs (lk_sharded_plan)"}
+    for (name, shapes, N) in (legs or THROUGHPUT_LEGS):
+        try:
+            out[name] = throughput_leg(torch, G, dev, comm, world, rank, dist, name, shapes, N)
+        except G.HipDeviceError as e:
+            out[name] = {"error": str(e)}
     return out
 
 

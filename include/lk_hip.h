@@ -225,6 +225,17 @@ void lk_debug_route_clear(void);
  * slabs, tile counters) of the current device was reallocated. Outgrown buffers are retired, never
  * freed before lk_shutdown, so HIP graphs captured earlier stay valid. */
 uint64_t lk_debug_scratch_epoch(void);
+/* Test hook: store `value` into split-K tile counter `index` of the gemm_q_* fallback GEMMs'
+ * scratch for (current device, stream), synchronously. Every split-K launch re-arms the counters
+ * it uses on its own stream first, so a poked (or otherwise stale) word never leaves a tile
+ * unwritten (round 4's failure mechanism). */
+int lk_debug_poke_gemm_counter(void *stream, int64_t index, int32_t value);
+/* Scratch lifetime: lk_scratch_release frees the batched kernels' scratch of
+ * (current device, stream), retired buffers included, after synchronising that stream; the caller
+ * guarantees that no HIP graph it will still replay captured a launch on that stream. lk_scratch_bytes
+ * = device bytes that scratch holds on the current device, all streams. */
+int lk_scratch_release(void *stream);
+uint64_t lk_scratch_bytes(void);
 
 /* ---- multi-GPU: row shards + RCCL all-gather over xGMI -----------------
  * The reference is single-device; this is the north star's partition of the same operator.
@@ -268,6 +279,11 @@ typedef struct lk_sharded_plan lk_sharded_plan;
 int lk_sharded_plan_create(lk_comm *comm, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
                            lk_sharded_plan **out);
 int lk_sharded_plan_launch(lk_sharded_plan *plan, void *stream);
+/* Throughput form: the local rows on `compute`, the node set's RCCL group of in-place all-gathers on
+ * `gather` behind an event of the local launch, so independent plans issued back to back overlap one
+ * plan's exchange with the next plan's rows (both streams on the communicator's device; capturable when
+ * the caller joins `gather` back into the capture's origin stream). */
+int lk_sharded_plan_launch_split(lk_sharded_plan *plan, void *compute_stream, void *gather_stream);
 int lk_sharded_plan_num_gathers(const lk_sharded_plan *plan);
 void lk_sharded_plan_destroy(lk_sharded_plan *plan);
 /* lk_sharded_plan_launch always issues its RCCL group, at one rank too (in-place copies), so the
@@ -315,9 +331,15 @@ void lk_p2p_plan_destroy(lk_p2p_plan *plan);
  * F32 [1, M] (N = 1 streaming nodes of one quant type), and every rank's dst tensors laid out alike
  * (one byte offset per pair of ranks over all nodes). Ranks on one device share its CUs and need
  * streams of their own (they wait for each other inside their launches). Waits are bounded like a
- * chain plan's: lk_p2p_chain_timed_out reports (and re-arms) a rank whose barrier gave up. On several
- * GPUs the dst buffers must be coherent for peer stores (fine-grained allocations); one-GPU tests run
- * P ranks on device 0. */
+ * chain plan's: lk_p2p_chain_timed_out reports (and re-arms) a rank whose barrier gave up.
+ * Memory model (round 6): arrival words in fine-grained device memory; the rank completing a stage
+ * issues a system-scope release before its cross adds, the poller a system-scope acquire after its
+ * poll, and the next stage loads its activations at system scope; each wave stores its rows to a peer
+ * as one contiguous store per block of 64 rows; a closing barrier ends every rank's launch only once
+ * every rank's last stage has drained, so a rank's dst is complete when that rank's stream is.
+ * Ranks on several GPUs are refused (LK_ERR_NOT_IMPLEMENTED) until a multi-GPU run validates this
+ * (LK_P2P_CHAIN_CROSS_DEVICE=1 opts in; the dst buffers must then be fine-grained allocations); the
+ * one-GPU tests run P ranks on device 0. */
 typedef struct lk_p2p_chain lk_p2p_chain;
 int lk_p2p_chain_create(lk_p2p_group *g, const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const int32_t *stage,
                         int n, lk_p2p_chain **out);
@@ -326,6 +348,8 @@ int lk_p2p_chain_create(lk_p2p_group *g, const lk_tensor *a, const lk_tensor *b,
 int lk_p2p_chain_launch(lk_p2p_chain *chain, void *const *streams);
 int lk_p2p_chain_timed_out(lk_p2p_chain *chain);
 uint64_t lk_p2p_chain_num_launches(const lk_p2p_chain *chain);
+/* The group's own stream of rank r (the one lk_p2p_chain_launch(chain, NULL) uses), or NULL. */
+void *lk_p2p_chain_rank_stream(lk_p2p_chain *chain, int r);
 void lk_p2p_chain_destroy(lk_p2p_chain *chain);
 
 /* ---- graph residency over host buffers ---------------------------------------

@@ -48,6 +48,7 @@ struct lk_sharded_plan {
   lk_plan *local = nullptr;                 // this rank's rows of every node: one grouped launch
   struct Gather { void *full; uint64_t chunk; };
   std::vector<Gather> gathers;             // per node: in-place all-gather of chunk bytes per rank
+  hipEvent_t rows_done = nullptr;          // lk_sharded_plan_launch_split: the local launch's completion
 };
 
 namespace {
@@ -182,13 +183,9 @@ int lk_sharded_plan_create(lk_comm *comm, const lk_tensor *a, const lk_tensor *b
 // the gathers are RCCL's (trivial) in-place copies, so the code path a multi-GPU node runs is the
 // one the one-GPU tests exercise. Inside an outer lk_comm_group_start / end (one thread driving
 // several devices) the gathers join that group.
-int lk_sharded_plan_launch(lk_sharded_plan *p, void *stream) {
-  if (!p) return lk_detail_fail(LK_ERR_INVALID_ARG, "null sharded plan");
-  hipStream_t st = (hipStream_t)stream;
-  if (!p->comm->comm) return lk_detail_fail(LK_ERR_DEVICE, "sharded plan: its communicator was aborted");
-  return on_device(p->comm->device, [&]() -> int {
-    int rc = lk_plan_launch(p->local, stream);
-    if (rc) return rc;
+namespace {
+// One RCCL group of the plan's in-place all-gathers on stream st (the plan's device current).
+int issue_gathers(lk_sharded_plan *p, hipStream_t st) {
     if (p->gathers.empty()) return LK_OK;
     NCCL_TRY(ncclGroupStart(), "ncclGroupStart");
     for (auto &g : p->gathers) {
@@ -205,6 +202,38 @@ int lk_sharded_plan_launch(lk_sharded_plan *p, void *stream) {
     }
     NCCL_TRY(ncclGroupEnd(), "ncclGroupEnd");
     return LK_OK;
+}
+}  // namespace
+
+int lk_sharded_plan_launch(lk_sharded_plan *p, void *stream) {
+  if (!p) return lk_detail_fail(LK_ERR_INVALID_ARG, "null sharded plan");
+  hipStream_t st = (hipStream_t)stream;
+  if (!p->comm->comm) return lk_detail_fail(LK_ERR_DEVICE, "sharded plan: its communicator was aborted");
+  return on_device(p->comm->device, [&]() -> int {
+    int rc = lk_plan_launch(p->local, stream);
+    if (rc) return rc;
+    return issue_gathers(p, st);
+  });
+}
+
+// Throughput form (round 6): the local rows on `compute`, the all-gathers on `gather` behind an event
+// of the local launch, so a caller issuing many independent plans overlaps plan i's exchange over xGMI
+// with plan i + 1's rows. Both streams on the communicator's device; graph-capturable (the event makes
+// `gather` part of a capture begun on `compute`; the caller joins it back before ending the capture).
+int lk_sharded_plan_launch_split(lk_sharded_plan *p, void *compute, void *gather) {
+  if (!p) return lk_detail_fail(LK_ERR_INVALID_ARG, "null sharded plan");
+  if (!p->comm->comm) return lk_detail_fail(LK_ERR_DEVICE, "sharded plan: its communicator was aborted");
+  return on_device(p->comm->device, [&]() -> int {
+    if (!p->rows_done && hipEventCreateWithFlags(&p->rows_done, hipEventDisableTiming) != hipSuccess) {
+      p->rows_done = nullptr;
+      return lk_detail_fail(LK_ERR_DEVICE, "sharded plan: event");
+    }
+    int rc = lk_plan_launch(p->local, compute);
+    if (rc) return rc;
+    if (hipEventRecord(p->rows_done, (hipStream_t)compute) != hipSuccess ||
+        hipStreamWaitEvent((hipStream_t)gather, p->rows_done, 0) != hipSuccess)
+      return lk_detail_fail(LK_ERR_DEVICE, "sharded plan: stream hand-off");
+    return issue_gathers(p, (hipStream_t)gather);
   });
 }
 
@@ -212,6 +241,7 @@ int lk_sharded_plan_num_gathers(const lk_sharded_plan *p) { return p ? (int)p->g
 
 void lk_sharded_plan_destroy(lk_sharded_plan *p) {
   if (!p) return;
+  if (p->rows_done) (void)on_device(p->comm->device, [&] { (void)hipEventDestroy(p->rows_done); return 0; });
   if (p->local) lk_plan_destroy(p->local);
   delete p;
 }

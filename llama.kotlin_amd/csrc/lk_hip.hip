@@ -128,7 +128,6 @@ State &S() {
   static State s;
   return s;
 }
-Dev &cur() { return S().devs[S().device < 0 ? 0 : S().device]; }
 
 int block_bytes(int32_t t) {
   switch (t) {
@@ -424,6 +423,7 @@ struct GemmScratch {
   unsigned *tcnt = nullptr;  // split-K arrival counters, one word per output tile of a launch
   size_t tcnt_n = 0;
   std::vector<void *> retired;
+  uint64_t retired_bytes = 0;
   uint64_t epoch = 0;
 };
 
@@ -460,7 +460,7 @@ int grow_scratch(GemmScratch &S, void **p, size_t *have, size_t want, bool zero,
     return fail(LK_ERR_DEVICE, "scratch: hipMalloc of %zu B failed", bytes);
   }
   if (zero) HIP_TRY(hipMemsetAsync(q, 0, bytes, st));
-  if (*p) S.retired.push_back(*p);
+  if (*p) { S.retired.push_back(*p); S.retired_bytes += *have; }
   *p = q;
   *have = bytes;
   S.epoch++;
@@ -493,6 +493,10 @@ int splitk_counters(int slices, size_t slab_bytes, int64_t ntiles, bool list_ok,
     S.tcnt = (unsigned *)p;
     S.tcnt_n = have / sizeof(unsigned);
   }
+  // re-armed on the launch stream before every launch (stream-ordered, captured with it): a word left
+  // non-zero by anything — a launch that failed part-way, a poke — cannot make a tile's last arrival
+  // fire early or never (the kernels re-arm it too)
+  HIP_TRY(hipMemsetAsync(S.tcnt, 0, (size_t)ntiles * kChainLine * sizeof(unsigned), st));
   *out = S.tcnt;
   return LK_OK;
 }
@@ -507,6 +511,10 @@ int gemm_counters(size_t tiles, hipStream_t st, int32_t **out) {
     S.counter = (int32_t *)p;
     S.counter_n = have / sizeof(int32_t);
   }
+  // re-armed before every launch (see splitk_counters): round 4's resident-graph failure was a tile
+  // whose counter was non-zero at entry, so its last arrival never fired and the tile stayed unwritten
+  // (DESIGN §4); tests/test_scratch_gpu.py pokes a counter through lk_debug_poke_gemm_counter
+  HIP_TRY(hipMemsetAsync(S.counter, 0, tiles * sizeof(int32_t), st));
   *out = S.counter;
   return LK_OK;
 }
@@ -1183,12 +1191,19 @@ int ensure_scratch(Dev &s, int idx, size_t bytes) {
 }
 
 // Lazily create the library stream on the caller's CURRENT device (a rank that
-// selected device r keeps device r).
-int ensure_init() {
+// selected device r keeps device r) and report that device. The host entry points work on the
+// device this returns — the calling thread's own HIP device — never on a process-wide field
+// another thread may change meanwhile (lk_mul_mat_sharded_at's P = 1 path used to
+// set S().device without the lock and leave it changed).
+int ensure_init(int *dev_out = nullptr) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  if (S().device == dev && S().devs[dev].stream) return LK_OK;
-  return lk_init(dev);
+  if (dev < 0 || dev >= kMaxDevices || !S().devs[dev].stream || !S().devs[dev].fail_flag) {
+    int rc = lk_init(dev);
+    if (rc) return rc;
+  }
+  if (dev_out) *dev_out = dev;
+  return LK_OK;
 }
 
 // The library stream of device d (created on first use); leaves d current.
@@ -1302,6 +1317,55 @@ const char *lk_last_error(void) { return g_err.c_str(); }
 const char *lk_debug_route(void) { return g_route.c_str(); }
 
 void lk_debug_route_clear(void) { g_route.clear(); }
+
+// Test hook: store `value` into gemm_q_*'s split-K tile counter `index` of the
+// (current device, stream) scratch, allocating the counters if needed; stream-ordered on `stream`.
+int lk_debug_poke_gemm_counter(void *stream, int64_t index, int32_t value) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  if (index < 0 || index >= (1 << 20)) return fail(LK_ERR_INVALID_ARG, "counter index %lld", (long long)index);
+  hipStream_t st = pick_stream(stream);
+  int32_t *ctr = nullptr;
+  if ((rc = gemm_counters((size_t)index + 1, st, &ctr))) return rc;
+  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(ctr + index), value, 1, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return LK_OK;
+}
+
+// Frees the batched-kernel scratch (activation fragments, split-K slabs, counters, retired buffers)
+// of (current device, stream) after synchronising that stream (the per-stream map never
+// shrank). The caller guarantees that no HIP graph it will replay captured a launch on that stream.
+int lk_scratch_release(void *stream) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(LK_ERR_DEVICE, "scratch release: no device");
+  hipStream_t st = pick_stream(stream);
+  HIP_TRY(hipStreamSynchronize(st));
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  auto it = scratch_map().find(ScratchKey{dev, st});
+  if (it == scratch_map().end()) return LK_OK;
+  GemmScratch &G = it->second;
+  for (void *p : G.retired) HIP_TRY(hipFree(p));
+  for (void *p : {G.frag, G.partial, (void *)G.counter, (void *)G.tcnt})
+    if (p) HIP_TRY(hipFree(p));
+  scratch_map().erase(it);
+  return LK_OK;
+}
+
+// Device bytes held by the batched-kernel scratch of the current device, all streams (live + retired).
+uint64_t lk_scratch_bytes(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  uint64_t t = 0;
+  for (auto &kv : scratch_map())
+    if (kv.first.dev == dev) {
+      const GemmScratch &G = kv.second;
+      t += G.frag_bytes + G.partial_bytes + G.counter_n * sizeof(int32_t) + G.tcnt_n * sizeof(unsigned) + G.retired_bytes;
+    }
+  return t;
+}
 
 uint64_t lk_debug_scratch_epoch(void) {
   int dev = 0;
@@ -1419,27 +1483,25 @@ int lk_mul_mat_device(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, vo
 }
 
 int lk_weights_pin(const lk_tensor *a, uint64_t generation) {
-  int rc = ensure_init();
+  int dev = 0;
+  int rc = ensure_init(&dev);
   if (rc) return rc;
   if (!a || !a->data) return fail(LK_ERR_NO_BUFFER, "Tensor buffer not found");
   const uint64_t bytes = pin_bytes(a);
   if (a->data_offset + bytes > a->buf_bytes) return fail(LK_ERR_OUT_OF_BOUNDS, "pin: tensor exceeds its buffer");
-  return pin_on(S().device, a, a->data_offset, bytes, generation);
+  return pin_on(dev, a, a->data_offset, bytes, generation);
 }
 
 // Host-buffer operator: the Kotlin drop-in. ByteArrays stay authoritative; A comes
 // from the residency cache when a current mirror covers its bytes (the latest generation
 // pinned over them: older ones were superseded), otherwise it is staged per call.
-int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
-  Checked c;
-  int rc = check(a, b, dst, &c);
-  if (rc) return rc;
-  if (c.empty) return LK_OK;
-  rc = ensure_init();
-  if (rc) return rc;
-  Dev &s = cur();
+namespace {
+// The host operator on device `dev` (current on this thread; its state initialised by the caller).
+int mul_mat_host_on(int dev, const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c) {
+  int rc = LK_OK;
+  Dev &s = S().devs[dev];
   hipStream_t st = s.stream;
-  const unsigned mark = fail_mark(S().device);
+  const unsigned mark = fail_mark(dev);
   const uint64_t a_bytes = c.a_hi - c.a_lo, b_bytes = c.b_hi - c.b_lo, d_bytes = c.d_hi - c.d_lo;
   // A: cached mirror or staged copy
   const MirrorRef pinned = find_pinned(s, a->data, c.a_lo, c.a_hi);  // held for the call
@@ -1469,7 +1531,18 @@ int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync((uint8_t *)dst->data + c.d_lo, s.scratch[2], d_bytes, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  return sync_failures(S().device, mark);
+  return sync_failures(dev, mark);
+}
+}  // namespace
+
+int lk_mul_mat(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst) {
+  Checked c;
+  int rc = check(a, b, dst, &c);
+  if (rc) return rc;
+  if (c.empty) return LK_OK;
+  int dev = 0;
+  if ((rc = ensure_init(&dev))) return rc;
+  return mul_mat_host_on(dev, a, b, dst, c);
 }
 
 // ---- row-sharded host operator: one process, several GPUs (SURVEY §8b lk_mul_mat_sharded) -----
@@ -1554,14 +1627,16 @@ int lk_mul_mat_sharded_at(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst
   const uint64_t ew = dst->type == LK_TYPE_F16 ? 2 : 4;
   const bool rows_ok = pitch && (uint64_t)(c.N - 1) * dst->nb[0] + ew <= dst->nb[1];
   const int P = rows_ok ? (int)std::min<int64_t>(n_shards, c.M) : 1;
-  if (P == 1) {  // one device: first_device's
+  if (P == 1) {  // one device: first_device's (explicitly: no process-wide device field is touched)
     int prev = 0;
     (void)hipGetDevice(&prev);
-    int rc1 = init_dev(first_device % ndev);
-    if (rc1 == LK_OK) {
-      S().device = first_device % ndev;
-      rc1 = lk_mul_mat(a, b, dst);
+    const int d = first_device % ndev;
+    int rc1;
+    {
+      std::lock_guard<std::mutex> lk(S().mu);  // init_dev creates the stream / flag once
+      rc1 = init_dev(d);
     }
+    if (rc1 == LK_OK) rc1 = mul_mat_host_on(d, a, b, dst, c);
     (void)hipSetDevice(prev);
     return rc1;
   }
@@ -1959,13 +2034,14 @@ int lk_plan_chain_timed_out(lk_plan *plan) {
 
 int lk_sync_timeouts(uint32_t *count) {
   if (!count) return fail(LK_ERR_INVALID_ARG, "null count");
-  int rc = ensure_init();
+  int dev = 0;
+  int rc = ensure_init(&dev);
   if (rc) return rc;
   unsigned v = 0;
   if (hipDeviceSynchronize() != hipSuccess) return fail(LK_ERR_DEVICE, "sync");
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(lk_sync_timeout_count), sizeof(v)) != hipSuccess)
     return fail(LK_ERR_DEVICE, "timeout count");
-  Dev &d = cur();  // the device count is monotonic: report the increase since the last call
+  Dev &d = S().devs[dev];  // the device count is monotonic: report the increase since the last call
   *count = v - d.timeouts_seen;
   d.timeouts_seen = v;
   return LK_OK;
@@ -2479,7 +2555,7 @@ int graph_compute_one(lk_graph *g) {
     if ((rc = graph_bind(g, false))) return rc;
     g->rebinds++;
   }
-  hipStream_t st = cur().stream;
+  hipStream_t st = S().devs[g->device].stream;
   auto enqueue = [&]() -> int {
     for (auto &x : g->h2d) HIP_TRY(hipMemcpyAsync(x.dev, g->staging + x.stage, x.bytes, hipMemcpyHostToDevice, st));
     for (size_t l = 0; l < g->levels.size(); l++)
@@ -2758,8 +2834,9 @@ int lk_dot_direct(int32_t kind, const lk_tensor *a, const lk_tensor *b, int64_t 
   if (rc) return rc;
   if (c.M <= 0 || c.N <= 0) return LK_OK;
   if (!out) return fail(LK_ERR_NO_BUFFER, "output buffer not found");
-  if ((rc = ensure_init())) return rc;
-  Dev &s = cur();
+  int dev = 0;
+  if ((rc = ensure_init(&dev))) return rc;
+  Dev &s = S().devs[dev];
   hipStream_t st = s.stream;
   const uint64_t a_bytes = c.a_hi - c.a_lo, b_bytes = c.b_hi - c.b_lo, o_bytes = (uint64_t)(c.M * c.N) * sizeof(float);
   if ((rc = ensure_scratch(s, 0, std::max<uint64_t>(a_bytes, 16)))) return rc;

@@ -617,7 +617,9 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
       for (int q = 0; q < 4; q++) {
         const int k = min(wave + kStreamWaves * (4 * r + q), xinst - 1), i = k * 64 + lane;
         const int p = min(i >> 4, NP - 1), t = (i & 15) ^ ((i >> 4) & 15);
-        xv[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (p * 16 + t) * 16, 0, 16));
+        // sc1 (aux 16) loads: another workgroup's write-through outputs; a multi-GPU rank loads at
+        // system scope (sc0 sc1, aux 17): some of those rows were stored by peers
+        xv[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (p * 16 + t) * 16, 0, PEER ? 17 : 16));
       }
     };
     auto x_store = [&](int r, const f32x4 (&xv)[4]) __attribute__((always_inline)) {
@@ -670,9 +672,16 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
           const unsigned top = __hip_atomic_fetch_add(bsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if constexpr (PEER) {  // this rank's stage is complete: tell every rank (itself included)
             const unsigned nsh = gridDim.x < 8 ? gridDim.x : 8;
-            if (top == nsh - 1)
+            if (top == nsh - 1) {
+              // every workgroup of this rank drained its stores (vmcnt(0)) before it arrived, and the
+              // rows went to the peers as system-scope stores: a system-scope release (L2 write-back)
+              // and an explicit drain before the cross adds, so no add can overtake them (the
+              // compiler may drop the fence's own wait: MI355X_MICROARCH.md, compiler hazard)
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
               for (int r = 0; r < peer->P; r++)
                 __hip_atomic_fetch_add(peer->cross[r] + (bar - 1) * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
           }
         }
       }
@@ -694,6 +703,13 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
             break;
           }
           __builtin_amdgcn_s_sleep(2);
+        }
+        if constexpr (PEER) {
+          // peers wrote this stage's activations into this rank's dst over the fabric: a system-scope
+          // acquire (L1 / non-coherent L2 lines invalidated), waited for before the barrier releases
+          // the other waves, whose loads below are system-scope too
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
       }
       LK_CS(2, __builtin_amdgcn_s_memrealtime());
@@ -798,6 +814,7 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
 #endif
     int slot = 0, u = 0;
     LK_GLOBAL float *out = (LK_GLOBAL float *)dst_node + (int64_t)r0 * dst_stride;
+    [[maybe_unused]] float peer_keep = 0.f;  // PEER: lane j holds row (64·k + j) of the wave's current block of 64
     for (int row = 0; row < nrows; row++) {
       float acc = 0.f;
 #pragma unroll
@@ -851,11 +868,21 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
       if (lane == 63) {
         if (sync) __hip_atomic_store(out + (int64_t)row * dst_stride, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
         else out[(int64_t)row * dst_stride] = tot;
-        if constexpr (PEER)  // the row into every other rank's copy of dst
-          for (int r = 0; r < peer->P; r++)
-            if (r != peer->rank)
-              __hip_atomic_store((LK_GLOBAL float *)((LK_GLOBAL uint8_t *)(out + (int64_t)row * dst_stride) + peer->delta[r]), tot,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if constexpr (PEER) {
+        // the rows into every other rank's copy of dst, one contiguous store per peer for each block of
+        // up to 64 of the wave's rows (dst is a dense [1, M] vector: lk_p2p_chain_create checks it)
+        // instead of a scattered 4-B system-scope store per row and peer
+        const float tb = __shfl(tot, 63, kWave);
+        if (lane == (row & 63)) peer_keep = tb;
+        if ((row & 63) == 63 || row == nrows - 1) {
+          const int base = row & ~63, cnt = row - base + 1;
+          if (lane < cnt)
+            for (int r = 0; r < peer->P; r++)
+              if (r != peer->rank)
+                __hip_atomic_store((LK_GLOBAL float *)((LK_GLOBAL uint8_t *)(out + (int64_t)(base + lane) * dst_stride) + peer->delta[r]),
+                                   peer_keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
       }
     }
     LK_CS(6, __builtin_amdgcn_s_memrealtime());
@@ -874,7 +901,27 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
       if (prev == gridDim.x - 1) {
         for (int b = lane; b <= nbar * 9; b += kWave) __hip_atomic_store(sync + b * kChainLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (PEER)
-          if (lane == 0) __hip_atomic_fetch_add(peer->epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) {
+            // closing barrier: every workgroup of this rank has drained its last stage's stores
+            // (its own and the peers'); the launch ends only once every rank's have, so a rank's dst is
+            // complete when its own stream is (line nbar of every rank's cross words; then the epoch)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int r = 0; r < peer->P; r++)
+              __hip_atomic_fetch_add(peer->cross[r] + nbar * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), bound = lk_sync_wait_bound;
+            unsigned *xw = peer->cross[peer->rank] + nbar * kChainLine;
+            while (__hip_atomic_load(xw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < cross_target) {
+              if (__builtin_amdgcn_s_memrealtime() - t0 >= bound) {
+                __hip_atomic_store(sync + (nbar * 9 + 1) * kChainLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lk_note_timeout();
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            __hip_atomic_fetch_add(peer->epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
       }
     }
   }

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -437,10 +438,25 @@ int lk_p2p_chain_create(lk_p2p_group *g, const lk_tensor *a, const lk_tensor *b,
   std::vector<int> share(P, 0);
   for (int r = 0; r < P; r++)
     for (int q = 0; q < P; q++) share[r] += g->dev[q] == g->dev[r];
-  const size_t lines = (size_t)std::max(c->nbar, 1) + 1;  // barrier lines + the epoch line
+  // Ranks on different GPUs: the memory model below (fine-grained arrival words, system-scope release
+  // before every cross add, system-scope acquire and loads after every poll, a closing barrier) has only
+  // run with every rank on one GPU, where one L2 hides any gap in it. Refused until a multi-GPU run
+  // validates it; LK_P2P_CHAIN_CROSS_DEVICE=1 opts in (unvalidated).
+  {
+    bool multi = false;
+    for (int r = 1; r < P; r++) multi |= g->dev[r] != g->dev[0];
+    static const bool cross_ok = [] { const char *e = std::getenv("LK_P2P_CHAIN_CROSS_DEVICE"); return e && *e == '1'; }();
+    if (multi && !cross_ok)
+      return lk_detail_fail(LK_ERR_NOT_IMPLEMENTED, "p2p chain: ranks on several GPUs are not validated yet (set "
+                                                    "LK_P2P_CHAIN_CROSS_DEVICE=1 to opt in); use lk_sharded_plan");
+  }
+  // per rank: one line per stage barrier, the closing barrier's line (nbar), the epoch line (nbar + 1);
+  // fine-grained device memory, so the peers' system-scope adds and this rank's polls meet coherently
+  const size_t lines = (size_t)c->nbar + 2;
   for (int r = 0; r < P; r++) {
     const int rc = on_device(g->dev[r], [&]() -> int {
-      if (hipMalloc((void **)&c->cross[r], lines * lk::kChainLine * sizeof(unsigned)) != hipSuccess) {
+      if (hipExtMallocWithFlags((void **)&c->cross[r], lines * lk::kChainLine * sizeof(unsigned), hipDeviceMallocFinegrained) !=
+          hipSuccess) {
         c->cross[r] = nullptr;
         return lk_detail_fail(LK_ERR_DEVICE, "p2p chain: out of device memory");
       }
@@ -558,6 +574,12 @@ int lk_p2p_chain_timed_out(lk_p2p_chain *c) {
 }
 
 uint64_t lk_p2p_chain_num_launches(const lk_p2p_chain *c) { return c ? c->launches : 0; }
+
+void *lk_p2p_chain_rank_stream(lk_p2p_chain *c, int r) {
+  if (!c || r < 0 || r >= c->g->P) return nullptr;
+  if (rank_streams(c->g)) return nullptr;
+  return (void *)c->g->rank_stream[r];
+}
 
 void lk_p2p_chain_destroy(lk_p2p_chain *c) {
   if (!c) return;

@@ -19,7 +19,7 @@ from ._lib import (HipDeviceError, IllegalArgumentException, IllegalStateExcepti
 from .backend import GGMLBackendRegistry, GGMLHipBackend, GGMLStatus
 from .ops import (DotKind, MulMatPlan, ResidentGraph, computeDotProductF32Q41, computeDotProductF32Q80, computeDotProductMatrix,
                   computeDotProductQ40Q40, computeDotProductQ41Q41, computeDotProductQ80Q40, computeDotProductQ80Q80, computeMatMul,
-                  computeMatMulSharded, dequantizeTensor, quantizeTensor, setSyncWaitBound, syncCountersSum, syncTimeouts, debugRoute, debugScratchEpoch, to_lk, validateMatMul, weightsCachedBytes, weightsCachedCount,
+                  computeMatMulSharded, dequantizeTensor, quantizeTensor, setSyncWaitBound, syncCountersSum, syncTimeouts, debugRoute, debugScratchEpoch, debugPokeGemmCounter, scratchRelease, scratchBytes, to_lk, validateMatMul, weightsCachedBytes, weightsCachedCount,
                   weightsEvict, weightsEvictAll, weightsEvictBuffer, weightsPin, weightsPinSharded)
 from .gguf import GGUFContext, GGUFParser, GGUFTensorInfo, GGUFType, LoadedModel, ModelLoader
 from .sharded import Comm, P2PChain, P2PGroup, P2PMulMatPlan, RowShardedMulMat, ShardedMulMatPlan, row_slice, shard_rows, shard_view
@@ -27,7 +27,7 @@ from .tensor import (GGMLCGraph, GGMLContext, GGMLGraphAllocator, GGMLOp, GGMLTe
                      calculateContiguousStrides, calculateTensorByteSize)
 
 __all__ = [
-    "syncTimeouts", "setSyncWaitBound", "syncCountersSum", "debugRoute", "debugScratchEpoch",
+    "syncTimeouts", "setSyncWaitBound", "syncCountersSum", "debugRoute", "debugScratchEpoch", "debugPokeGemmCounter", "scratchRelease", "scratchBytes",
     "GGMLType", "GGMLTensor", "GGMLGraphAllocator", "GGMLContext", "GGMLCGraph", "GGMLOp",
     "calculateContiguousStrides", "calculateTensorByteSize",
     "computeMatMul", "computeMatMulSharded", "weightsPinSharded", "validateMatMul", "MulMatPlan", "ResidentGraph", "dequantizeTensor", "quantizeTensor", "weightsPin",

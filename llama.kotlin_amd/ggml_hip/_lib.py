@@ -77,7 +77,8 @@ EXPORTED_SYMBOLS = (
     "lk_mul_mat_sharded_at", "lk_weights_pin_sharded_at",
     "lk_plan_create", "lk_plan_launch", "lk_plan_num_launches", "lk_plan_destroy", "lk_plan_create_chain",
     "lk_plan_chain_timed_out", "lk_sync_timeouts", "lk_set_sync_wait_bound", "lk_sync_counters_sum",
-    "lk_debug_route", "lk_debug_route_clear", "lk_debug_scratch_epoch",
+    "lk_debug_route", "lk_debug_route_clear", "lk_debug_scratch_epoch", "lk_debug_poke_gemm_counter",
+    "lk_scratch_release", "lk_scratch_bytes",
     "lk_graph_create", "lk_graph_create_sharded", "lk_graph_num_sharded", "lk_graph_compute",
     "lk_graph_num_levels", "lk_graph_num_launches",
     "lk_graph_transfer_bytes", "lk_graph_destroy", "lk_graph_num_rebinds",
@@ -86,11 +87,11 @@ EXPORTED_SYMBOLS = (
     "lk_comm_unique_id", "lk_comm_init_rank", "lk_comm_init_all", "lk_comm_nranks", "lk_comm_rank",
     "lk_comm_device", "lk_comm_num_collectives",
     "lk_comm_destroy", "lk_comm_abort", "lk_comm_group_start", "lk_comm_group_end",
-    "lk_sharded_plan_create", "lk_sharded_plan_launch", "lk_sharded_plan_num_gathers", "lk_sharded_plan_destroy",
+    "lk_sharded_plan_create", "lk_sharded_plan_launch", "lk_sharded_plan_launch_split", "lk_sharded_plan_num_gathers", "lk_sharded_plan_destroy",
     "lk_p2p_group_create", "lk_p2p_group_nranks", "lk_p2p_group_destroy", "lk_p2p_plan_create", "lk_p2p_plan_launch",
     "lk_p2p_plan_num_launches", "lk_p2p_plan_signal", "lk_p2p_plan_destroy",
     "lk_p2p_chain_create", "lk_p2p_chain_launch", "lk_p2p_chain_timed_out", "lk_p2p_chain_num_launches",
-    "lk_p2p_chain_destroy",
+    "lk_p2p_chain_destroy", "lk_p2p_chain_rank_stream",
     "lk_dequantize_device", "lk_quantize_device", "lk_dot_direct", "lk_dot_direct_device",
     # include/lk_gguf.h
     "lk_gguf_open_memory", "lk_gguf_open_file", "lk_gguf_close", "lk_gguf_version", "lk_gguf_alignment",
@@ -143,6 +144,10 @@ def load():
         L.lk_debug_route.restype = ctypes.c_char_p
         L.lk_debug_route_clear.restype = None
         L.lk_debug_scratch_epoch.restype = ctypes.c_uint64
+    if hasattr(L, "lk_scratch_release"):  # (absent from round-5 lab builds loaded for A/B)
+        L.lk_debug_poke_gemm_counter.argtypes = [vp, ctypes.c_int64, ctypes.c_int32]
+        L.lk_scratch_release.argtypes = [vp]
+        L.lk_scratch_bytes.restype = ctypes.c_uint64
     L.lk_plan_num_launches.argtypes = [vp]
     L.lk_plan_destroy.argtypes = [vp]
     L.lk_plan_destroy.restype = None
@@ -178,6 +183,8 @@ def load():
         L.lk_comm_abort.argtypes = [vp]
     L.lk_sharded_plan_create.argtypes = [vp, P, P, P, ctypes.c_int, ctypes.POINTER(vp)]
     L.lk_sharded_plan_launch.argtypes = [vp, vp]
+    if hasattr(L, "lk_sharded_plan_launch_split"):  # (absent from round-5 lab builds loaded for A/B)
+        L.lk_sharded_plan_launch_split.argtypes = [vp, vp, vp]
     L.lk_sharded_plan_num_gathers.argtypes = [vp]
     L.lk_sharded_plan_destroy.argtypes = [vp]
     L.lk_sharded_plan_destroy.restype = None
@@ -200,6 +207,9 @@ def load():
         L.lk_p2p_chain_num_launches.argtypes = [vp]
         L.lk_p2p_chain_num_launches.restype = ctypes.c_uint64
         L.lk_p2p_chain_destroy.argtypes = [vp]
+        if hasattr(L, "lk_p2p_chain_rank_stream"):
+            L.lk_p2p_chain_rank_stream.argtypes = [vp, ctypes.c_int]
+            L.lk_p2p_chain_rank_stream.restype = vp
         L.lk_p2p_chain_destroy.restype = None
     L.lk_dequantize_device.argtypes = [P, vp, vp]
     L.lk_quantize_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp]

@@ -396,5 +396,28 @@ def debugScratchEpoch() -> int:
     return int(_lib.load().lk_debug_scratch_epoch())
 
 
-__all__ = ["syncTimeouts", "setSyncWaitBound", "syncCountersSum", "debugRoute", "debugScratchEpoch", "computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
+def _stream_ptr(stream=None) -> int:
+    """The HIP stream handle launches requested with `stream` go to (_OnStream's choice)."""
+    return int(_OnStream(stream).stream.cuda_stream)
+
+
+def debugPokeGemmCounter(index: int, value: int, stream=None) -> None:
+    """Store `value` into the gemm_q_* split-K tile counter `index` of the (current device, stream)
+    scratch (lk_debug_poke_gemm_counter): a test of the re-arm every split-K launch does first."""
+    _lib.check(_lib.load().lk_debug_poke_gemm_counter(_stream_ptr(stream), int(index), int(value)))
+
+
+def scratchRelease(stream=None) -> None:
+    """Free the batched kernels' scratch of (current device, stream) (lk_scratch_release); no HIP graph
+    that will still be replayed may have captured a launch on that stream."""
+    _lib.check(_lib.load().lk_scratch_release(_stream_ptr(stream)))
+
+
+def scratchBytes() -> int:
+    """Device bytes of batched-kernel scratch on the current device, all streams (lk_scratch_bytes)."""
+    return int(_lib.load().lk_scratch_bytes())
+
+
+__all__ = ["syncTimeouts", "setSyncWaitBound", "syncCountersSum", "debugRoute", "debugScratchEpoch",
+           "debugPokeGemmCounter", "scratchRelease", "scratchBytes", "computeMatMul", "computeMatMulSharded", "ResidentGraph", "weightsPinSharded", "validateMatMul", "MulMatPlan", "dequantizeTensor", "quantizeTensor", "weightsPin",
            "weightsEvictAll", "weightsEvict", "weightsEvictBuffer", "weightsCachedBytes", "weightsCachedCount", "to_lk", "GGMLCGraph", "calculateTensorByteSize"]

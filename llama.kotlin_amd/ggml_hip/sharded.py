@@ -235,6 +235,13 @@ class ShardedMulMatPlan:
         with _OnStream(stream) as sh:
             _lib.check(_lib.load().lk_sharded_plan_launch(self._handle, sh))
 
+    def launchSplit(self, compute, gather):
+        """Throughput form (lk_sharded_plan_launch_split): the local rows on torch stream `compute`,
+        the all-gathers on `gather` behind them, so the next plan's rows overlap this exchange. The
+        caller joins `gather` back (compute.wait_stream(gather)) before it reads the outputs."""
+        from . import _lib
+        _lib.check(_lib.load().lk_sharded_plan_launch_split(self._handle, int(compute.cuda_stream), int(gather.cuda_stream)))
+
     def close(self):
         if self._handle:
             from . import _lib
@@ -379,6 +386,15 @@ class P2PChain:
         P = self.group.nranks
         hs = (ctypes.c_void_p * P)(*[int(s.cuda_stream) for s in streams])
         _lib.check(_lib.load().lk_p2p_chain_launch(self._handle, hs))
+
+    def rankStream(self, r: int):
+        """The group's own stream of rank r (what launch() uses) as a torch ExternalStream."""
+        import torch
+        from . import _lib
+        h = _lib.load().lk_p2p_chain_rank_stream(self._handle, int(r))
+        if not h:
+            _lib.check(_lib.LK_ERR_DEVICE)
+        return torch.cuda.ExternalStream(h, device=torch.device("cuda", self.group.devices[r]))
 
     def timedOut(self) -> bool:
         """True if any rank's barrier gave up waiting (synchronizes the ranks' devices; re-arms)."""

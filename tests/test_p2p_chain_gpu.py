@@ -8,7 +8,7 @@ weights, bit for bit (each row is the same wave's sequential sum either way)."""
 import numpy as np
 import pytest
 
-from _util import random_acts, random_weights
+from _util import parity_ok, random_acts, random_weights
 
 pytestmark = pytest.mark.gpu
 
@@ -47,19 +47,38 @@ def _nodes(w, t, layers, a_of):
     return nodes, stages
 
 
+def _weights(G, ga, oracle, layers, seed):
+    wbuf = ga.addBuffer(layers * 7 * F * H * 18 // 32 + 4096)
+    w, qb, off = {}, {}, 0
+    for L in range(layers):
+        for i, (name, m, k, _) in enumerate(LAYER):
+            w[f"{name}{L}"] = G.GGMLTensor(G.GGMLType.Q4_0, [k, m], bufferId=wbuf, dataOffset=off)
+            qb[f"{name}{L}"] = oracle.quantize(2, random_weights(m * k, 100 * L + i + seed))
+            ga.setTensorBytes(w[f"{name}{L}"], qb[f"{name}{L}"])
+            off += (m * k // 32 * 18 + 255) // 256 * 256
+    return w, qb
+
+
+def _oracle_each_node(ga, oracle, qb, t, layers):
+    """Every node of the stage-by-stage reference against the oracle on that node's own GPU input
+    (core/GGMLComputeOps.kt:120-145 restated in oracle/), at the §8c bar."""
+    def vec(name):
+        return np.frombuffer(ga.tensorBytes(t[name]).cpu().numpy().tobytes(), np.float32)
+    for L in range(layers):
+        for (name, m, k, src) in LAYER:
+            x = vec("x0" if (src == "x" and L == 0) else f"down{L - 1}" if src == "x" else f"{src}{L}")
+            ref = oracle.mat_mul_q(2, qb[f"{name}{L}"], m, k, x.reshape(k, 1)).reshape(m)
+            ok, msg = parity_ok(vec(f"{name}{L}").reshape(m, 1), ref.reshape(m, 1))
+            assert ok, (name, L, msg)
+
+
 @pytest.mark.parametrize("P", [1, 2, 4])
 def test_p2p_chain_ranks_on_one_gpu(gpu, oracle, P):
     import torch
     import ggml_hip as G
     layers = 2
     ga = G.GGMLGraphAllocator(defaultBufferSize=16)
-    wbuf = ga.addBuffer(layers * 7 * F * H * 18 // 32 + 4096)
-    w, off = {}, 0
-    for L in range(layers):
-        for i, (name, m, k, _) in enumerate(LAYER):
-            w[f"{name}{L}"] = G.GGMLTensor(G.GGMLType.Q4_0, [k, m], bufferId=wbuf, dataOffset=off)
-            ga.setTensorBytes(w[f"{name}{L}"], oracle.quantize(2, random_weights(m * k, 100 * L + i + P)))
-            off += (m * k // 32 * 18 + 255) // 256 * 256
+    w, qb = _weights(G, ga, oracle, layers, P)
     act_bytes = 4 * (H + layers * sum(m for (_, m, _, _) in LAYER)) + 256 * (1 + 7 * layers)
     x0 = random_acts(H, 5 + P)
     # reference: the whole weights, stage by stage
@@ -71,6 +90,7 @@ def test_p2p_chain_ranks_on_one_gpu(gpu, oracle, P):
         G.MulMatPlan(ga, [nd for nd, sg in zip(nodes, stages) if sg == st]).launch(stream=s)
     torch.cuda.synchronize()
     want = {k: ga.tensorBytes(v).cpu().numpy().tobytes() for k, v in ref.items()}
+    _oracle_each_node(ga, oracle, qb, ref, layers)  # the stage-by-stage reference is itself on the oracle
     # P ranks, each with its own activation buffer of the same layout
     ranks, acts = [], []
     for r in range(P):
@@ -123,4 +143,77 @@ def test_p2p_chain_refuses_a_shared_stream_and_uneven_layouts(gpu, oracle):
     with pytest.raises(G.NotOffloadedError):  # rank 1's two dsts sit at another offset than rank 0's
         G.P2PChain(group, ga, [[(G.shard_view(a, 2, r), xs[r], ds[r]), (G.shard_view(a, 2, r), xs[r], [d2[0], d_off][r])]
                                for r in range(2)], [0, 0])
+    group.close()
+
+
+def test_p2p_chain_back_to_back_without_host_sync(gpu, oracle):
+    """a rank's launch used to end while peers' last-stage rows to its dst could still be in
+    flight. With the closing barrier, syncing ONE rank's own stream makes its dst complete. Two ranks
+    on device 0, three launches back to back with new inputs enqueued on each rank's stream between
+    them (no host sync), then each rank's stream alone is synchronised and its dst read from a separate
+    non-blocking stream: equal to the stage-by-stage reference of the last inputs, on the oracle."""
+    import torch
+    import ggml_hip as G
+    P, layers = 2, 2
+    ga = G.GGMLGraphAllocator(defaultBufferSize=16)
+    w, qb = _weights(G, ga, oracle, layers, 17)
+    act_bytes = 4 * (H + layers * sum(m for (_, m, _, _) in LAYER)) + 256 * (1 + 7 * layers)
+    xs = [torch.from_numpy(random_acts(H, 30 + i)).cuda() for i in range(3)]
+    ref = _activations(G, ga, ga.addBuffer(act_bytes), layers)
+    ga.setTensorBytes(ref["x0"], xs[-1].cpu().numpy())
+    nodes, stages = _nodes(w, ref, layers, lambda a: a)
+    s = torch.cuda.Stream()
+    for st in range(max(stages) + 1):
+        G.MulMatPlan(ga, [nd for nd, sg in zip(nodes, stages) if sg == st]).launch(stream=s)
+    torch.cuda.synchronize()
+    want = {k: ga.tensorBytes(v).cpu().numpy().tobytes() for k, v in ref.items()}
+    _oracle_each_node(ga, oracle, qb, ref, layers)
+    ranks, acts = [], []
+    for r in range(P):
+        t = _activations(G, ga, ga.addBuffer(act_bytes), layers)
+        for k, v in t.items():
+            ga.setTensorBytes(v, np.full(4 * v.ne[1], 0xFF, np.uint8))
+        ranks.append(_nodes(w, t, layers, lambda a, r=r: G.shard_view(a, P, r))[0])
+        acts.append(t)
+    group = G.P2PGroup([0] * P)
+    chain = G.P2PChain(group, ga, ranks, stages)
+    rs = [chain.rankStream(r) for r in range(P)]
+    torch.cuda.synchronize()
+    for x in xs:
+        for r in range(P):  # rank r's input, stream-ordered before its launch
+            with torch.cuda.stream(rs[r]):
+                ga.tensorBytes(acts[r]["x0"]).copy_(x.view(torch.uint8))
+        chain.launch()
+    reader = torch.cuda.Stream()
+    for r in range(P):
+        rs[r].synchronize()  # this rank alone
+        with torch.cuda.stream(reader):
+            got = {k: ga.tensorBytes(v).clone() for k, v in acts[r].items()}
+        reader.synchronize()
+        for k, v in got.items():
+            assert v.cpu().numpy().tobytes() == want[k], (r, k)
+    torch.cuda.synchronize()
+    assert not chain.timedOut()
+    assert chain.numLaunches == 3
+    chain.close()
+    group.close()
+
+
+def test_p2p_chain_refuses_ranks_on_several_gpus_until_validated(gpu, oracle):
+    """the cross-GPU memory model has never run on two GPUs, so a chain whose ranks
+    span devices is refused (LK_ERR_NOT_IMPLEMENTED) unless LK_P2P_CHAIN_CROSS_DEVICE=1. Needs two
+    visible GPUs (skipped on the one-GPU box)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU: ranks on several devices cannot be built here")
+    import ggml_hip as G
+    ga = G.GGMLGraphAllocator(defaultBufferSize=16)
+    a = G.GGMLTensor(G.GGMLType.Q4_0, [256, 64], bufferId=ga.addBuffer(64 * 256 // 32 * 18 + 256))
+    ga.setTensorBytes(a, oracle.quantize(2, random_weights(64 * 256, 1)))
+    bufs = [ga.addBuffer(4096), ga.addBuffer(4096)]
+    xs = [G.GGMLTensor(G.GGMLType.F32, [1, 256], bufferId=b) for b in bufs]
+    ds = [G.GGMLTensor(G.GGMLType.F32, [1, 64], bufferId=b, dataOffset=1024) for b in bufs]
+    group = G.P2PGroup([0, 1])
+    with pytest.raises(G.NotOffloadedError):
+        G.P2PChain(group, ga, [[(G.shard_view(a, 2, r), xs[r], ds[r])] for r in range(2)], [0])
     group.close()

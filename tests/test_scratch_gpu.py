@@ -204,3 +204,74 @@ def test_split_k_behind_a_busy_null_stream(gpu, oracle):
         _check_oracle(oracle, 2, q, M, K, x, got)
     torch.cuda.synchronize()
     assert G.syncCountersSum() == 0
+
+
+@pytest.mark.parametrize("value", [1, 5, 11, 1000])
+def test_poked_tile_counter_is_rearmed(gpu, oracle, value):
+    """VERDICT r5 item 6, the round-4 mechanism made a directed test: a gemm_q_* split-K tile counter
+    set non-zero before the call (lk_debug_poke_gemm_counter) must never leave a tile unwritten — the
+    library re-arms the counters it uses on the launch stream before every split-K launch. Device
+    buffers on an explicit stream (the poke and the call are stream-ordered), result on the oracle, no
+    all-zero tile, counters zero after."""
+    import torch
+    import ggml_hip as G
+    qt, M, K, N = 2, 128 * 6, 384, 4  # the graph test's down-projection geometry: 12 K slices per tile
+    q = oracle.quantize(qt, random_weights(M * K, 80 + value))
+    x = random_acts(K * N, 81 + value).reshape(K, N)
+    ref = oracle.mat_mul_q(qt, q, M, K, x)
+    dga = G.GGMLGraphAllocator(device="cuda", defaultBufferSize=16)
+    a = G.GGMLTensor(G.GGMLType.Q4_0, [K, M], bufferId=dga.addBuffer(q.size + 256))
+    b = G.GGMLTensor(G.GGMLType.F32, [N, K], bufferId=dga.addBuffer(4 * K * N + 256))
+    d = G.GGMLTensor(G.GGMLType.F32, [N, M], bufferId=dga.addBuffer(4 * M * N + 256))
+    dga.setTensorBytes(a, q)
+    dga.setTensorBytes(b, np.ascontiguousarray(x))
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    tiles = 0
+    for rep in range(3):  # unpoked (learns the tile count), every tile poked, tile 0 alone poked
+        for t in range(tiles if rep == 1 else min(tiles, 1) if rep == 2 else 0):
+            G.debugPokeGemmCounter(t, value, stream=s)
+        dga.setTensorBytes(d, np.zeros(4 * M * N, np.uint8))
+        torch.cuda.synchronize()
+        G.debugRoute()
+        G.computeMatMul(dga, None, a, b, d, stream=s)
+        s.synchronize()
+        route = G.debugRoute()
+        m = re.search(r"gemm_q_\w+<[^>]*>:t(\d+)s(\d+)", route)
+        assert m and int(m.group(2)) > 1, route  # the split-K route with tile counters
+        tiles = int(m.group(1))
+        got = dga.tensorBytes(d).cpu().numpy().view(np.float32).reshape(M, N)
+        assert not any((got[t:t + 64] == 0).all() for t in range(0, M, 64)), (value, route)
+        ok, msg = parity_ok(got, ref, noise=noise_for(oracle, qt, q, M, K, x))
+        assert ok, (value, rep, route, msg)
+    assert G.syncCountersSum() == 0
+
+
+def test_scratch_release_frees_a_streams_scratch(gpu, oracle):
+    """scratch per (device, stream) never shrank. lk_scratch_release frees one
+    stream's scratch; calls on that stream afterwards allocate afresh and stay right."""
+    import torch
+    import ggml_hip as G
+    qt, M, K, N = 2, 512, 4096, 256  # wide GEMM: activation fragments + split-K slabs
+    q = oracle.quantize(qt, random_weights(M * K, 90))
+    x = random_acts(K * N, 91).reshape(K, N)
+    ref = oracle.mat_mul_q(qt, q, M, K, x, tight=True, threads=16)
+    dga = G.GGMLGraphAllocator(device="cuda", defaultBufferSize=16)
+    a = G.GGMLTensor(G.GGMLType.Q4_0, [K, M], bufferId=dga.addBuffer(q.size + 256))
+    b = G.GGMLTensor(G.GGMLType.F32, [N, K], bufferId=dga.addBuffer(4 * K * N + 256))
+    d = G.GGMLTensor(G.GGMLType.F32, [N, M], bufferId=dga.addBuffer(4 * M * N + 256))
+    dga.setTensorBytes(a, q)
+    dga.setTensorBytes(b, np.ascontiguousarray(x))
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    base = G.scratchBytes()
+    for rep in range(2):
+        G.computeMatMul(dga, None, a, b, d, stream=s)
+        s.synchronize()
+        held = G.scratchBytes()
+        assert held > base, (rep, held, base)
+        got = dga.tensorBytes(d).cpu().numpy().view(np.float32).reshape(M, N)
+        ok, msg = parity_ok(got, ref, noise=noise_for(oracle, qt, q, M, K, x))
+        assert ok, (rep, msg)
+        G.scratchRelease(stream=s)
+        assert G.scratchBytes() == base, (rep, G.scratchBytes(), base)
