@@ -741,10 +741,14 @@ def throughput_leg(torch, G, dev, comm, world, rank, dist, name, shapes, N, reps
     ref = wf @ xk
     err = (got[rows].double() - ref).abs()
     scale = ref.abs().max().clamp_min(1e-30)
-    rel = float((err / torch.maximum(ref.abs(), 1e-3 * scale)).max())
+    # the §8c bar of tests/_util.py parity_ok: 1e-3 of max(|r|, 1e-3·‖r‖∞), or the f32 accumulation
+    # noise 4·√K·2⁻²⁴·Σ|w||x| (+ 2⁻¹⁷·Σ|w||x| for the batched path's bf16 hi/lo activation split)
+    noise = (4.0 * K ** 0.5 * 2.0 ** -24 + (2.0 ** -17 if N > 1 else 0.0)) * (wf.abs() @ xk.abs())
+    allow = torch.maximum(1e-3 * torch.maximum(ref.abs(), 1e-3 * scale), noise)
+    rel = max(float((err / allow).max()) * 1e-3, float(err.max() / scale))  # <= 1e-3 passes
     if keep is not None:  # tests: the first call's operands and gathered output, on the host
         keep.update(q=full_q[0].cpu().numpy(), x=xk.float().cpu().numpy(), got=got.cpu().numpy().copy(), M=M, K=K)
-    out["check"] = {"rows_checked": len(rows), "max_rel_err": rel, "bar": 1e-3, "ok": bool(rel <= 1e-3) and same,
+    out["check"] = {"rows_checked": len(rows), "err_vs_bar": rel, "bar": 1e-3, "ok": bool(rel <= 1e-3) and same,
                     "checksum_equal_on_every_rank": same,
                     "against": "float64 dot products of dequantizeTensor's weights, rows sampled from every shard"}
     for p in sharded + local:

@@ -25,6 +25,7 @@
 #include "lk_kernels.hpp"
 #include "lk_skinny.hpp"
 #include "lk_kpart.hpp"
+#include "lk_wide32.hpp"
 #include "../../include/lk_gguf.h"
 
 using namespace lk;
@@ -942,6 +943,76 @@ int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
   return LK_OK;
 }
 
+// Q4_0 / Q4_1 at N > 16 on gemm_w32_kernel (round 6, lk_wide32.hpp): K % 128 == 0, rows 8-B aligned, the
+// last row's last window (OVERREAD bytes past the matrix) inside A's buffer, 32-bit DMA and slab offsets.
+bool w32_eligible(const lk_tensor *a, const Checked &c) {
+  static const bool off = getenv("LK_W32_OFF") != nullptr;  // A/B only: back to the round-5 kernels
+  if (off || (a->type != LK_TYPE_Q4_0 && a->type != LK_TYPE_Q4_1) || c.N <= 16 || c.K % 128) return false;
+  const uintptr_t base = (uintptr_t)a->data + a->data_offset;
+  const uint64_t bb = a->type == LK_TYPE_Q4_1 ? 20 : 18;
+  const uint64_t over = a->type == LK_TYPE_Q4_1 ? W32Geom<LK_TYPE_Q4_1, 4, 2>::OVERREAD : W32Geom<LK_TYPE_Q4_0, 4, 2>::OVERREAD;
+  const uint64_t rb = (uint64_t)(c.K / 32) * bb, ntx = (uint64_t)(c.N + 31) / 32, nblk = (uint64_t)c.K / 32;
+  return base % 8 == 0 && (uint64_t)c.M * rb < (1ull << 32) && ntx * nblk * 4096 < (1ull << 32) &&
+         nblk * ntx * 32 * 4 < (1ull << 32) && c.a_hi + over <= a->buf_bytes;
+}
+
+template <int QT, int MT, int NT>
+int launch_w32_t(W32Args g, hipStream_t st) {
+  using W = W32Geom<QT, MT, NT>;
+  g.tiles_m = (g.M + W::BM - 1) / W::BM;
+  g.tiles_n = (g.N + W::BN - 1) / W::BN;
+  const int tiles = g.tiles_m * g.tiles_n, nst = g.K / 128, cus = cu_count();
+  // one workgroup per CU (~132-140 KB of LDS): split K over workgroups only when the tiles leave CUs
+  // idle, at most as many slices as fit the CUs, each at least 4 stages
+  int slices = std::max(1, std::min({cus / std::max(tiles, 1), nst / 4, 16}));
+  g.sstages = (nst + slices - 1) / slices;
+  slices = (nst + g.sstages - 1) / g.sstages;
+  g.slices = slices;
+  g.tasks = tiles * slices;
+  if (slices > 1) {
+    GemmScratch &S = gemm_scratch(st);
+    const size_t pb = (size_t)slices * tiles * W::BM * W::BN * sizeof(float);
+    if (pb >= (1ull << 31)) { g.slices = 1; g.sstages = nst; g.tasks = tiles; slices = 1; }
+    else {
+      if (int rc = grow(S, &S.partial, &S.partial_bytes, pb)) return rc;
+      g.partial = (float *)S.partial;
+      if (int rc = splitk_counters(slices, pb, tiles, true, true, st, &g.tcnt)) return rc;
+      if (!g.tcnt) return fail(LK_ERR_DEVICE, "w32: no split-K counters");
+    }
+  }
+  const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
+  note_route("w32<%d,%d,%d>:t%ds%d", QT, MT, NT, tiles, slices);
+  hipLaunchKernelGGL((gemm_w32_kernel<QT, MT, NT>), dim3(grid), dim3(W::NW * 64), W::LDS, st, g);
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+int launch_w32(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  GemmScratch &S = gemm_scratch(st);
+  const int64_t nblk = c.K / 32, ntx = (c.N + 31) / 32;
+  const size_t fb = (size_t)ntx * nblk * 4 * 1024, tb = (size_t)nblk * ntx * 32 * sizeof(float);
+  int rc = grow(S, &S.frag, &S.frag_bytes, fb + tb);
+  if (rc) return rc;
+  XSplit32Args xa{};
+  xa.b = (const uint8_t *)b->data + b->data_offset;
+  xa.b_nb0 = b->nb[0]; xa.b_nb1 = b->nb[1];
+  xa.N = (int32_t)c.N; xa.K = (int32_t)c.K;
+  xa.frag = (u32x4 *)S.frag;
+  xa.tsum = (float *)((uint8_t *)S.frag + fb);
+  xa.mult = a->type == LK_TYPE_Q4_1 ? -128.f : -136.f;
+  W32Args g{};
+  g.a = (const uint8_t *)a->data + a->data_offset;
+  g.frag = xa.frag;
+  g.tsum = xa.tsum;
+  g.dst = (uint8_t *)dst->data + dst->data_offset;
+  g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
+  g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
+  hipLaunchKernelGGL(xsplit32_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  const bool q41 = a->type == LK_TYPE_Q4_1;
+  if (c.N > 32) return q41 ? launch_w32_t<LK_TYPE_Q4_1, 4, 2>(g, st) : launch_w32_t<LK_TYPE_Q4_0, 4, 2>(g, st);
+  return q41 ? launch_w32_t<LK_TYPE_Q4_1, 3, 1>(g, st) : launch_w32_t<LK_TYPE_Q4_0, 3, 1>(g, st);
+}
+
 int launch_gemm(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
   GemmScratch &S = gemm_scratch(st);
   const int64_t nblk = c.K / 32, ntx = (c.N + 15) / 16;
@@ -1175,7 +1246,10 @@ int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *ds
   static const bool no_f32_mfma = getenv_flag("LK_NO_F32_MFMA");
   if (c.path == Path::kF32 && !no_f32_mfma) return launch_f32_mfma(a, b, dst, c, st);
   if (gemv_eligible(a, b, dst, c)) return run_single_gemv(a, b, dst, c, st);
-  if (gemm_eligible(c)) return skinny_eligible(a, c) ? launch_skinny(a, b, dst, c, st) : launch_gemm(a, b, dst, c, st);
+  if (gemm_eligible(c)) {
+    if (w32_eligible(a, c)) return launch_w32(a, b, dst, c, st);
+    return skinny_eligible(a, c) ? launch_skinny(a, b, dst, c, st) : launch_gemm(a, b, dst, c, st);
+  }
   return launch_generic(a, b, dst, c, st);
 }
 

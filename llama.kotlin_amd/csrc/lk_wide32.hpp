@@ -1,0 +1,393 @@
+// lk_wide32.hpp — Q4_0 / Q4_1 x F32 at N > 16 on v_mfma_f32_32x32x16_bf16, one wave per SIMD
+// (round 6): config C5 (4096 x 4096, batch 512) and the skinny config C3 (11008 x 4096, batch 32).
+//
+// Arithmetic (the reference's, K/core/GGMLComputeOps.kt:70-145, within the F32 bar): per 32-weight block
+// b of row m and activation column n, with the codes as exact bf16 128 + q and x = hi + lo in bf16 pairs
+// (|x − hi − lo| ≤ 2⁻¹⁷|x|), the MFMA chain gives p = Σ_k (128 + q_k)·x_k + T with the C input
+// T = −c·Σ_k (hi + lo)_k (c = 136 for Q4_0: p = Σ (q − 8)·x; c = 128 for Q4_1: p = Σ q·x), then
+// acc += d·p (Q4_1: + m·Σx = (−m/128)·T) in f32 with the block's f16 scale d, so an Inf / NaN scale gives
+// what d·p gives (tests/test_gpu_parity.py::test_w32_route_and_nonfinite_scales).
+//
+// Why this shape: gemm_wide_kernel (8 waves, 16x16x32, 256 x 64 tiles, K split in
+// two) was LDS-read bound — per 16-cycle MFMA ~480 B of LDS reads (x fragments re-read by every row tile
+// of a wave, 4-way-conflicting ds_read_b32 weight reads, T as 1 KB per block and column tile) — and its
+// two K slices wrote 16 MB of slabs at C5. Here:
+//   * a workgroup is BM = 32·MT rows x BN = 32·NT columns, 4 waves (one per SIMD: a wave owns the SIMD's
+//     512 registers and hides its ~5 VALU per MFMA behind the matrix pipe, MI355X_MICROARCH.md);
+//   * the 4 waves split each 4-block stage's K: wave g takes block g over the FULL tile (MT x NT chains
+//     of 32 x 32), so every fragment and weight byte in LDS is read by exactly one wave and a decoded
+//     weight fragment feeds NT column tiles;
+//   * 32x32x16: an MFMA holds the SIMD's issue for 8 of its 32 cycles (16x16x32: 8 of 16), leaving room
+//     for the decode (7 VALU per 8 codes) and the 16 scale FMAs per chain and block;
+//   * C layout: one weight row per lane (col = lane & 31), so the block scale is a per-lane scalar; T is
+//     16 values per lane, broadcast ds_read_b128 from a 1-KB stage slot;
+//   * weights: each row's 4-block window (72 / 80 B in 5 16-B pieces) by LDS-DMA; a lane reads the two
+//     pieces holding its block (conflict-free ds_read_b128 at the 5-piece pitch) and aligns its 8 code
+//     bytes in registers;
+//   * the 4 K groups are summed through LDS in group order (deterministic); with `slices` > 1 (K split
+//     over workgroups, C3's shapes) each slice stores its partial write-through and the last to arrive
+//     at the tile's counter sums the slabs in slice order (no waits);
+//   * blockIdx -> task XCD-aware: each XCD takes a contiguous run of tasks, column tile major.
+namespace lk {
+
+struct W32Args {
+  const uint8_t *a;      // weights (buffer base + dataOffset), rows of K/32 blocks
+  const u32x4 *frag;     // xsplit32_kernel: [ntx32][nblk][step 2][split 2][64 lanes] x 16 B
+  const float *tsum;     // xsplit32_kernel: [nblk][ntx32·32] = −c·Σ_block (hi + lo)
+  uint8_t *dst;
+  int64_t d_nb0, d_nb1;
+  int32_t M, N, K;
+  int32_t tiles_m, tiles_n, tasks;
+  int32_t slices, sstages;   // split K: slice s covers stages [s·sstages, (s + 1)·sstages)
+  float *partial;            // [slices][tiles][BM·BN] (slices > 1), lane-major per chain
+  unsigned *tcnt;            // per-tile arrival counters (kChainLine apart), zero between launches
+};
+
+template <int QT, int MT_, int NT_> struct W32Geom {
+  static constexpr int NW = 4, MT = MT_, NT = NT_, BM = 32 * MT, BN = 32 * NT, SB = 4;
+  static constexpr int BB = QT == LK_TYPE_Q4_1 ? 20 : 18;
+  static constexpr int WIN = 80;                            // bytes per row per stage (4 blocks: 72 / 80 B)
+  static constexpr int WP = WIN / 16;                       // 16-B pieces per row
+  static constexpr int W_INST = (BM * WP + 63) / 64;        // weight DMA instructions
+  static constexpr int X_INST = NT * SB * 4;                // 1-KB fragments (2 steps x hi/lo)
+  static constexpr int INST = W_INST + X_INST + 1;          // + T (SB x BN floats)
+  static constexpr int CW = (INST + NW - 1) / NW;           // per wave (the rest padding)
+  static constexpr int X_OFF = W_INST * 1024, T_OFF = X_OFF + X_INST * 1024, PAD_OFF = T_OFF + 1024;
+  static constexpr int STAGE = NW * CW * 1024;
+  static constexpr int D0 = (160 * 1024) / STAGE;
+  static constexpr int D = D0 > 5 ? 5 : D0;                 // ring slots (D − 2 stages in flight ahead)
+  static constexpr int LDS = D * STAGE;
+  static constexpr int OVERREAD = WIN - SB * BB;            // bytes a row's last window reads past it
+  static constexpr int CHAINS = MT * NT;
+  static_assert(STAGE >= PAD_OFF + 1024, "stage layout");
+  static_assert(D >= 3 && (D - 2) * CW < 64, "ring");
+  static_assert(CHAINS * NW * 4096 <= LDS, "K-group reduction buffer ([chain][group] x 4 KB)");
+  static_assert(4 * BN <= 1024, "T slot");
+};
+
+struct XSplit32Args {
+  const uint8_t *b;      // B(n, k) at n·nb0 + k·nb1
+  int64_t b_nb0, b_nb1;
+  int32_t N, K;
+  u32x4 *frag;
+  float *tsum;
+  float mult;            // −136 (Q4_0) or −128 (Q4_1)
+};
+
+// One wave per (32-column tile t, block kb); lane (n = lane & 31, h = lane >> 5) writes, for step s,
+// x(n, 32kb + 8(2h + s) + ord[j]) (ord = 0,4,1,5,2,6,3,7: q4_codes_128's element order of code dword
+// 2h + s) split into bf16 hi (truncated) and lo (x − hi rounded to nearest even), as fragment
+// ((t·nblk + kb)·2 + s)·2 + {0: hi, 1: lo}; and T = mult·Σ (hi + lo) over the block's 32 k.
+__global__ __launch_bounds__(256) void xsplit32_kernel(XSplit32Args g) {
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int64_t nblk = g.K / 32, ntx = (g.N + 31) / 32, item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= ntx * nblk) return;
+  const int64_t t = item / nblk, kb = item % nblk;
+  const int64_t n = 32 * t + (lane & 31);
+  float v[2][8];
+#pragma unroll
+  for (int s = 0; s < 2; s++)
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int64_t k = 32 * kb + 8 * (2 * h + s) + ((j >> 1) + 4 * (j & 1));
+      v[s][j] = n < g.N ? *(const float *)(g.b + n * g.b_nb0 + k * g.b_nb1) : 0.f;
+    }
+  float sum = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      uint32_t hb[2], lb[2];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t bx = __builtin_bit_cast(uint32_t, v[s][j + q]);
+        const float hf = __builtin_bit_cast(float, bx & 0xFFFF0000u);
+        const float r = v[s][j + q] - hf;  // exact
+        uint32_t br = __builtin_bit_cast(uint32_t, r);
+        br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even (r is finite, |r| < 2^-7·|x|)
+        hb[q] = bx;
+        lb[q] = br;
+        sum += hf + __builtin_bit_cast(float, br & 0xFFFF0000u);
+      }
+      hi[j / 2] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+      lo[j / 2] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+    }
+    u32x4 *f = g.frag + ((item * 2 + s) * 2) * 64 + lane;
+    f[0] = u32x4{hi[0], hi[1], hi[2], hi[3]};
+    f[64] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+  }
+  sum += __shfl_xor(sum, 32, kWave);
+  if (h == 0) g.tsum[kb * (ntx * 32) + n] = g.mult * sum;
+}
+
+// Block G of a stage window, from its two 16-B pieces G, G + 1 (window bytes [16G, 16G + 32); the block
+// starts at BB·G): the code dwords of lane half h for steps 0 and 1 (code bytes [8h, 8h + 8) of the
+// block), the scale d and (Q4_1) the min m.
+template <int QT, int G>
+__device__ __forceinline__ void w32_block(const u32x4 &p0, const u32x4 &p1, int h, uint32_t &c0, uint32_t &c1, float &d,
+                                          float &mn) {
+  const uint32_t Q[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+  if constexpr (QT == LK_TYPE_Q4_1) {  // 20-B blocks at 4G: d, m, codes all dword-aligned
+    c0 = h ? Q[G + 3] : Q[G + 1];
+    c1 = h ? Q[G + 4] : Q[G + 2];
+    d = h2f(Q[G] & 0xFFFFu);
+    mn = h2f(Q[G] >> 16);
+  } else {
+    constexpr int o = 2 * G + 2;  // first code byte, relative to the pieces
+    if constexpr ((o & 3) == 0) {  // G odd: code dwords aligned
+      constexpr int a = o / 4;
+      c0 = h ? Q[a + 2] : Q[a];
+      c1 = h ? Q[a + 3] : Q[a + 1];
+    } else {  // G even: two bytes off
+      constexpr int a = o / 4;
+      const uint32_t l0 = __builtin_amdgcn_alignbit(Q[a + 1], Q[a], 16), l1 = __builtin_amdgcn_alignbit(Q[a + 2], Q[a + 1], 16);
+      const uint32_t u0 = __builtin_amdgcn_alignbit(Q[a + 3], Q[a + 2], 16), u1 = __builtin_amdgcn_alignbit(Q[a + 4], Q[a + 3], 16);
+      c0 = h ? u0 : l0;
+      c1 = h ? u1 : l1;
+    }
+    constexpr int db = 2 * G;  // scale bytes
+    d = h2f((Q[db / 4] >> (8 * (db & 3))) & 0xFFFFu);
+    mn = 0.f;
+  }
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int QT, int MT, int NT, int G>
+__device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm, int tn, int st0, int st1,
+                                         f32x16 (&acc)[MT][NT]) {
+  using W = W32Geom<QT, MT, NT>;
+  constexpr int D = W::D, CW = W::CW;
+  const int lane = threadIdx.x & 63, wave = G, h = lane >> 5, m = lane & 31;
+  const int nblk = g.K / 32, ntx = (g.N + 31) / 32, n32 = ntx * 32;
+  const int64_t RB = (int64_t)nblk * W::BB;
+  const int nst = st1 - st0;
+  // per-lane DMA offsets from each instruction's stage base (fixed for the launch)
+  uint32_t vofs[CW];
+  int kind[CW];  // 0 weights, 1 fragments, 2 T, 3 padding (wave-uniform)
+#pragma unroll
+  for (int c = 0; c < CW; c++) {
+    const int q = wave * CW + c;
+    if (q < W::W_INST) {
+      const int p = min(q * 64 + lane, W::BM * W::WP - 1), r = p / W::WP, pc = p % W::WP;  // past the last piece: re-read it
+      const int64_t row = min((int64_t)tm * W::BM + r, (int64_t)g.M - 1);
+      vofs[c] = (uint32_t)(row * RB + pc * 16);
+      kind[c] = 0;
+    } else if (q < W::W_INST + W::X_INST) {
+      const int f = q - W::W_INST, j = f / (W::SB * 4), b = (f / 4) % W::SB, s = (f / 2) % 2, sp = f % 2;
+      const int64_t xt = min(tn * NT + j, ntx - 1);
+      vofs[c] = (uint32_t)(((((xt * nblk + b) * 2 + s) * 2 + sp) * 64 + lane) * 16);
+      kind[c] = 1;
+    } else if (q == W::W_INST + W::X_INST) {
+      const int b = min(lane / (W::BN / 4), W::SB - 1), c4 = lane % (W::BN / 4);  // lanes past 4 x BN: never read
+      const int col = min(tn * W::BN + 4 * c4, n32 - 4);
+      vofs[c] = (uint32_t)(((int64_t)b * n32 + col) * 4);
+      kind[c] = 2;
+    } else {
+      vofs[c] = 0;
+      kind[c] = 3;
+    }
+  }
+  auto issue = [&](int st, int sl) __attribute__((always_inline)) {
+    const int kb = (st0 + min(st, nst - 1)) * W::SB;  // past the last stage: reload it (never read)
+    const uint8_t *bw = g.a + (int64_t)kb * W::BB;
+    const uint8_t *bx = (const uint8_t *)g.frag + (int64_t)kb * 4 * 1024;
+    const uint8_t *bt = (const uint8_t *)(g.tsum + (int64_t)kb * n32);
+    uint8_t *slot = smem + sl * W::STAGE;
+#pragma unroll
+    for (int c = 0; c < CW; c++) {
+      const int q = wave * CW + c;
+      const uint8_t *base = kind[c] == 0 ? bw : kind[c] == 1 ? bx : bt;
+      uint8_t *to = kind[c] == 3 ? slot + W::PAD_OFF : slot + q * 1024;
+      dma16<false>(base, vofs[c], to);
+    }
+  };
+  // D − 1 stages in flight at the start; stage st's slot is refilled with stage st + D − 1 one stage later
+#pragma unroll
+  for (int st = 0; st < D - 1; st++) issue(st, st);
+  for (int st = 0; st < nst; st++) {
+    wait_vmcnt<(D - 2) * CW>();    // this wave's DMAs of stage st have landed (D − 2 younger stages may not)
+    __builtin_amdgcn_s_barrier();  // ... every wave's; and every wave is done reading stage st − 1's slot
+    asm volatile("" ::: "memory");
+    issue(st + D - 1, (st + D - 1) % D);  // refill the slot stage st − 1 used
+    const uint8_t *S = smem + (st % D) * W::STAGE;
+    // operands of block G: weights (two pieces per row tile), fragments, T
+    u32x4 wp[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; i++) {
+      const uint8_t *rp = S + (i * 32 + m) * W::WIN + G * 16;
+      wp[i][0] = *(const u32x4 *)rp;
+      wp[i][1] = *(const u32x4 *)(rp + 16);
+    }
+    bf16x8 xh[NT][2], xl[NT][2];
+#pragma unroll
+    for (int j = 0; j < NT; j++)
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        const u32x4 *fp = (const u32x4 *)(S + W::X_OFF + ((((j * W::SB + G) * 2 + s) * 2) * 1024)) + lane;
+        xh[j][s] = __builtin_bit_cast(bf16x8, fp[0]);
+        xl[j][s] = __builtin_bit_cast(bf16x8, fp[64]);
+      }
+    f32x16 T[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const float *tp = (const float *)(S + W::T_OFF) + G * W::BN + 32 * j + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const f32x4 v = *(const f32x4 *)(tp + 8 * q);
+        T[j][4 * q] = v.x; T[j][4 * q + 1] = v.y; T[j][4 * q + 2] = v.z; T[j][4 * q + 3] = v.w;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MT; i++) {
+      uint32_t c0, c1;
+      float d, mn;
+      w32_block<QT, G>(wp[i][0], wp[i][1], h, c0, c1, d, mn);
+      const bf16x8 w0 = q4_codes_128(c0), w1 = q4_codes_128(c1);
+      [[maybe_unused]] const float mq = mn * -0.0078125f;  // Q4_1: m·Σx = (−m/128)·T, exact
+#pragma unroll
+      for (int j = 0; j < NT; j++) {
+        f32x16 p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[j][0], w0, T[j], 0, 0, 0);
+        p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[j][0], w0, p, 0, 0, 0);
+        p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[j][1], w1, p, 0, 0, 0);
+        p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[j][1], w1, p, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          if constexpr (QT == LK_TYPE_Q4_1) acc[i][j][r] = fmaf(mq, T[j][r], acc[i][j][r]);
+          acc[i][j][r] = fmaf(d, p[r], acc[i][j][r]);
+        }
+      }
+    }
+  }
+  wait_vmcnt<0>();  // the padding stages, before the ring is reused for the reduction
+}
+
+template <int QT, int MT, int NT>
+__global__ __launch_bounds__(256, 1) void gemm_w32_kernel(W32Args g) {
+  using W = W32Geom<QT, MT, NT>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // task order (speed only: dispatch is observed round-robin over the 8 XCDs): workgroup b runs task
+  // (b % 8)·(grid / 8) + b / 8; tasks are column tile major, then row tile, then slice, so an XCD walks
+  // the row tiles of one column tile (its activation fragments stay in the XCD's L2)
+  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+  if (task >= g.tasks) return;  // grid padding
+  const int slice = task % g.slices, tile = task / g.slices;
+  const int tn = tile / g.tiles_m, tm = tile % g.tiles_m;
+  const int nst = g.K / 32 / W::SB;
+  const int st0 = slice * g.sstages, st1 = min(st0 + g.sstages, nst);
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+  if (st1 > st0) {
+    switch (wave) {  // K group = wave: its block's offsets are compile-time constants
+      case 0: w32_main<QT, MT, NT, 0>(g, smem, tm, tn, st0, st1, acc); break;
+      case 1: w32_main<QT, MT, NT, 1>(g, smem, tm, tn, st0, st1, acc); break;
+      case 2: w32_main<QT, MT, NT, 2>(g, smem, tm, tn, st0, st1, acc); break;
+      default: w32_main<QT, MT, NT, 3>(g, smem, tm, tn, st0, st1, acc); break;
+    }
+  }
+  // K groups summed in group order: chain c = i·NT + j is finished by wave c % 4; every wave parks its
+  // other chains in LDS ([chain][group] x 4 KB, lane-major float4s)
+  __syncthreads();
+  f32x4 *red = (f32x4 *)smem;
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      if ((i * NT + j) % 4 == wave) continue;
+      f32x4 *o = red + ((i * NT + j) * 4 + wave) * 256 + lane;
+#pragma unroll
+      for (int q = 0; q < 4; q++) o[q * 64] = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+    }
+  __syncthreads();
+  f32x4 sum[(W::CHAINS + 3) / 4][4];  // this wave's chains, summed over the K groups
+#pragma unroll
+  for (int i = 0; i < MT; i++)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const int c = i * NT + j;
+      if (c % 4 != wave) continue;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int gk = 0; gk < 4; gk++) {
+          const f32x4 p = gk == wave ? f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}
+                                     : red[(c * 4 + gk) * 256 + q * 64 + lane];
+          if (gk == 0) v = p;  // group 0 as is (0 + x would turn −0.0 into +0.0)
+          else { v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w; }
+        }
+        sum[c / 4][q] = v;
+      }
+    }
+  auto store_chain = [&](int c, const f32x4 (&s)[4]) __attribute__((always_inline)) {
+    const int i = c / NT, j = c % NT;
+    const int64_t mrow = (int64_t)tm * W::BM + 32 * i + (lane & 31);
+    if (mrow >= g.M) return;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int n0 = tn * W::BN + 32 * j + 8 * q + 4 * h;  // C rows 8q + 4h .. + 3 of the chain
+      uint8_t *o = g.dst + mrow * g.d_nb1 + (int64_t)n0 * g.d_nb0;
+      if (g.d_nb0 == 4 && n0 + 4 <= g.N && (((uintptr_t)o) & 15) == 0) {
+        *(f32x4 *)o = s[q];
+      } else {
+        const float e[4] = {s[q].x, s[q].y, s[q].z, s[q].w};
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (n0 + u < g.N) *(float *)(o + u * g.d_nb0) = e[u];
+      }
+    }
+  };
+  if (g.slices == 1) {
+#pragma unroll
+    for (int c = wave; c < W::CHAINS; c += 4) store_chain(c, sum[c / 4]);
+    return;
+  }
+  // split K: this slice's tile written through (sc1), every wave drained, one agent-scope arrival; the
+  // last slice to arrive sums the slabs in slice order (its own from registers) with sc1 loads and stores
+  // (splitk_arrive re-arms the counter). Nobody waits for another workgroup.
+  const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
+  const int64_t slab = (int64_t)W::BM * W::BN;  // floats per tile
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, (int)((int64_t)g.slices * tiles * slab * 4), 0x00020000);
+  auto at = [&](int sl, int c, int q) __attribute__((always_inline)) {  // a lane's float4 of chain c
+    return (int)((((int64_t)sl * tiles + tile) * slab + ((int64_t)c * 4 + q) * 256 + 4 * lane) * 4);
+  };
+#pragma unroll
+  for (int c = wave; c < W::CHAINS; c += 4)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sum[c / 4][q]), prs, at(slice, c, q), 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int *flag = (int *)smem + 64 * 1024 / 4;  // past the reduction buffer's chains read above
+  if (threadIdx.x == 0) *flag = splitk_arrive(g.tcnt + (int64_t)tile * kChainLine, (unsigned)g.slices) ? 1 : 0;
+  __syncthreads();
+  asm volatile("" ::: "memory");
+  if (!*flag) return;
+#pragma unroll
+  for (int c = wave; c < W::CHAINS; c += 4) {
+    f32x4 t[4];
+    for (int sl = 0; sl < g.slices; sl++) {
+      f32x4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        v[q] = sl == slice ? sum[c / 4][q] : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, at(sl, c, q), 0, 16));
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (sl == 0) t[q] = v[q];
+        else { t[q].x += v[q].x; t[q].y += v[q].y; t[q].z += v[q].z; t[q].w += v[q].w; }
+      }
+    }
+    store_chain(c, t);
+  }
+}
+
+}  // namespace lk

@@ -412,6 +412,30 @@ def test_wide_gemm_vs_oracle(gpu, oracle, qt, shape):
     assert ok, ("strided dst", msg)
 
 
+def test_w32_route_and_nonfinite_scales(gpu, oracle):
+    """Q4_0 at N > 32 runs gemm_w32_kernel (round 6, lk_wide32.hpp), which applies each block's f16
+    scale d to the block's MFMA sum in f32 (acc += d·p). Kotlin multiplies d into every term
+    ((d·(q − 8))·x, GGMLComputeOps.kt:120-145), so a non-finite scale makes the row's outputs
+    non-finite in both; they may differ only in which non-finite value (NaN vs ±Inf). Checked: the
+    route; finite-ness equal to the oracle element by element; every finite element on the oracle."""
+    import ggml_hip as G
+    M, K, N = 256, 1024, 64
+    q, x = make_inputs(oracle, 2, M, K, N, seed=99)
+    q = q.copy()
+    rb = K // 32 * 18
+    for row, blk, bits in ((3, 5, 0x7C00), (100, 0, 0x7E00), (200, 31, 0xFC00)):  # +Inf, NaN, -Inf
+        q[row * rb + blk * 18:row * rb + blk * 18 + 2] = np.frombuffer(np.uint16(bits).tobytes(), np.uint8)
+    ref = oracle.mat_mul_q(2, q, M, K, x, tight=True)
+    G.debugRoute()
+    got = gpu_matmul(2, q, M, K, N, x)
+    assert "w32" in G.debugRoute()
+    assert np.array_equal(np.isfinite(got), np.isfinite(ref))
+    fin = np.isfinite(ref).all(axis=1)
+    assert fin.sum() == M - 3
+    ok, msg = parity_ok(got[fin], ref[fin], noise=noise_for(oracle, 2, q, M, K, x)[fin])
+    assert ok, msg
+
+
 @pytest.mark.parametrize("shape", [(100, 1024, 36), (33, 128, 4), (257, 384, 60), (64, 4096, 32)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_f32_lds_kernel_edges(gpu, oracle, shape):

@@ -66,7 +66,8 @@ ROUTES = [
     (2, 4096, 4096, 8, "kpart"),        # two K slices added into dst
     (2, 11008, 4096, 32, "pair"),       # eight slices, reduce launch
     (6, 4096, 4096, 8, "skinny"),       # Q8_0
-    (2, 4096, 4096, 64, "wide"),        # last arriver per tile (tcnt)
+    (3, 4096, 4096, 64, "wide"),        # Q4_1: last arriver per tile (tcnt)
+    (2, 4096, 4096, 64, "w32"),         # Q4_0 at N > 32: no split K since round 6
     (3, 96, 1184, 40, "gemm_q_mfma"),   # Q4_1, 37 blocks per row: neither wide- nor LDS-eligible
 ]
 
