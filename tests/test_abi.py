@@ -55,7 +55,7 @@ PRODUCT_KERNELS = {
     "gemm_q_lds_kernel", "gemm_q_mfma_kernel", "kquant_n1_kernel", "kquant_nc_kernel",
     "kquant_gemv_kernel", "kquant_mul_mat_kernel", "mul_mat_generic_kernel", "dequantize_coop_kernel",
     "quantize_coop_kernel", "dequantize_kernel", "quantize_kernel", "dot_direct_kernel",
-    "repack_q4_kernel", "gemv_stream_peer_kernel",
+    "repack_q4_kernel", "gemv_stream_peer_kernel", "gemm_w32_kernel", "xsplit32_kernel",
 }
 
 
