@@ -950,15 +950,15 @@ bool w32_eligible(const lk_tensor *a, const Checked &c) {
   if (off || (a->type != LK_TYPE_Q4_0 && a->type != LK_TYPE_Q4_1) || c.N <= 16 || c.K % 128) return false;
   const uintptr_t base = (uintptr_t)a->data + a->data_offset;
   const uint64_t bb = a->type == LK_TYPE_Q4_1 ? 20 : 18;
-  const uint64_t over = a->type == LK_TYPE_Q4_1 ? W32Geom<LK_TYPE_Q4_1, 4, 2>::OVERREAD : W32Geom<LK_TYPE_Q4_0, 4, 2>::OVERREAD;
+  const uint64_t over = a->type == LK_TYPE_Q4_1 ? W32Geom<LK_TYPE_Q4_1, 2, 2, 2>::OVERREAD : W32Geom<LK_TYPE_Q4_0, 2, 2, 2>::OVERREAD;
   const uint64_t rb = (uint64_t)(c.K / 32) * bb, ntx = (uint64_t)(c.N + 31) / 32, nblk = (uint64_t)c.K / 32;
   return base % 8 == 0 && (uint64_t)c.M * rb < (1ull << 32) && ntx * nblk * 4096 < (1ull << 32) &&
          nblk * ntx * 32 * 4 < (1ull << 32) && c.a_hi + over <= a->buf_bytes;
 }
 
-template <int QT, int MT, int NT>
+template <int QT, int MT, int NT, int MH>
 int launch_w32_t(W32Args g, hipStream_t st) {
-  using W = W32Geom<QT, MT, NT>;
+  using W = W32Geom<QT, MT, NT, MH>;
   g.tiles_m = (g.M + W::BM - 1) / W::BM;
   g.tiles_n = (g.N + W::BN - 1) / W::BN;
   const int tiles = g.tiles_m * g.tiles_n, nst = g.K / 128, cus = cu_count();
@@ -981,8 +981,8 @@ int launch_w32_t(W32Args g, hipStream_t st) {
     }
   }
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
-  note_route("w32<%d,%d,%d>:t%ds%d", QT, MT, NT, tiles, slices);
-  hipLaunchKernelGGL((gemm_w32_kernel<QT, MT, NT>), dim3(grid), dim3(W::NW * 64), W::LDS, st, g);
+  note_route("w32<%d,%d,%d,%d>:t%ds%d", QT, MT, NT, MH, tiles, slices);
+  w32_launch(QT, MT, NT, MH, g, grid, W::LDS, st);
   HIP_TRY(hipGetLastError());
   return LK_OK;
 }
@@ -1007,10 +1007,14 @@ int launch_w32(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Che
   g.dst = (uint8_t *)dst->data + dst->data_offset;
   g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
-  hipLaunchKernelGGL(xsplit32_kernel, dim3((unsigned)((ntx * nblk + 3) / 4)), dim3(256), 0, st, xa);
+  w32_launch_xsplit(xa, (unsigned)((ntx * nblk + 3) / 4), st);
   const bool q41 = a->type == LK_TYPE_Q4_1;
-  if (c.N > 32) return q41 ? launch_w32_t<LK_TYPE_Q4_1, 4, 2>(g, st) : launch_w32_t<LK_TYPE_Q4_0, 4, 2>(g, st);
-  return q41 ? launch_w32_t<LK_TYPE_Q4_1, 3, 1>(g, st) : launch_w32_t<LK_TYPE_Q4_0, 3, 1>(g, st);
+  static const int cfg = [] { const char *e = getenv("LK_W32_CFG"); return e ? atoi(e) : 0; }();  // A/B only
+  if (c.N > 32) {
+    if (cfg == 1) return q41 ? launch_w32_t<LK_TYPE_Q4_1, 4, 2, 1>(g, st) : launch_w32_t<LK_TYPE_Q4_0, 4, 2, 1>(g, st);
+    return q41 ? launch_w32_t<LK_TYPE_Q4_1, 2, 2, 2>(g, st) : launch_w32_t<LK_TYPE_Q4_0, 2, 2, 2>(g, st);
+  }
+  return q41 ? launch_w32_t<LK_TYPE_Q4_1, 3, 1, 1>(g, st) : launch_w32_t<LK_TYPE_Q4_0, 3, 1, 1>(g, st);
 }
 
 int launch_gemm(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {

@@ -997,6 +997,7 @@ struct XSplitArgs {
 // used. One item per wave is the fastest measured (C5 55.6 vs 57.3 us with four: 16 waves per CU
 // in flight beat 4 waves with 32 loads each).
 constexpr int kXsItems = 1;
+#ifndef LK_W32_KERNELS  // (lk_w32.hip includes this header for its helpers only)
 __global__ __launch_bounds__(256) void xsplit_kernel(XSplitArgs g) {
   if (g.zero && (int)blockIdx.x >= g.xblocks) {  // dst zeroing: 4 columns of one row per thread
     const int c4 = (g.zN + 3) / 4;
@@ -1066,6 +1067,7 @@ __global__ __launch_bounds__(256) void xsplit_kernel(XSplitArgs g) {
     if (lane < 16) g.xsum[kb * (ntx * 16) + n] = g.mult * part;
   }
 }
+#endif
 
 // bf16 codes 128 + n of the 8 nibbles of dword u, slots in k order (0,4,1,5,2,6,3,7).
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t o) {
@@ -1331,6 +1333,14 @@ __device__ __forceinline__ void dma16(const void *sbase, uint32_t vofs, const vo
   sbase = (const void *)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo);
   if constexpr (NT) asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
   else asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+// The same with the LDS destination as a wave-uniform LDS address (no generic-pointer cast per call).
+__device__ __forceinline__ void dma16m(const void *sbase, uint32_t vofs, uint32_t m0) {
+  const uint64_t sb = (uint64_t)(uintptr_t)sbase;
+  const uint32_t sb_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
+  const uint32_t sb_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+  sbase = (const void *)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo);
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(vofs), "s"(sbase), "s"(m0) : "memory", "m0");
 }
 #pragma clang diagnostic pop
 
@@ -2712,6 +2722,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
 }
 
 // dst(n, m) = Σ_s P[s][m][n], slices in order (deterministic); one thread per 4 columns.
+#ifndef LK_W32_KERNELS  // (lk_w32.hip includes this header for its helpers only)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restrict__ P, int slices, int M, int N, int N16,
                                                             uint8_t *__restrict__ dst, int64_t d_nb0, int64_t d_nb1) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -2743,6 +2754,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restr
   for (int q = 0; q < 4; q++)
     if (n0 + q < N) *(float *)(dst + m * d_nb1 + (n0 + q) * d_nb0) = e4[q];
 }
+#endif
 
 // ---- F32 x F32 -> F32 general path on the f32 MFMA (computeMatMul :1530-1543, config C1) ----
 //
@@ -2808,6 +2820,7 @@ __global__ __launch_bounds__(256) void f32_mfma_kernel(GenericArgs g) {
 // K % 128 == 0, A rows and B k rows 16-B aligned, N % 4 == 0; rows / columns past M / N re-read
 // the last valid ones and are never stored.
 constexpr int kF32Chunk = 128;  // k per wave and chunk
+#ifndef LK_W32_KERNELS  // (lk_w32.hip includes this header for its helpers only)
 __global__ __launch_bounds__(256) void f32_lds_kernel(GenericArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2863,6 +2876,7 @@ __global__ __launch_bounds__(256) void f32_lds_kernel(GenericArgs g) {
     if (ii < g.M && jj < g.N) *(float *)(g.dst + jj * g.d_nb0 + ii * g.d_nb1) = v;
   }
 }
+#endif
 
 // ---- generic path (any K, any byte strides, ragged blocks) ----------------------
 

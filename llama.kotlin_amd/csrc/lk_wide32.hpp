@@ -28,6 +28,13 @@
 //     over workgroups, C3's shapes) each slice stores its partial write-through and the last to arrive
 //     at the tile's counter sums the slabs in slice order (no waits);
 //   * blockIdx -> task XCD-aware: each XCD takes a contiguous run of tasks, column tile major.
+#ifndef LK_W32_PK
+#define LK_W32_PK 1  // packed scale FMAs (lab: 0 = scalar)
+#endif
+#ifndef LK_W32_SCHED
+#define LK_W32_SCHED 0  // lab: VALU instructions per MFMA enforced by sched_group_barrier (0: the compiler's order)
+#endif
+
 namespace lk {
 
 struct W32Args {
@@ -43,8 +50,9 @@ struct W32Args {
   unsigned *tcnt;            // per-tile arrival counters (kChainLine apart), zero between launches
 };
 
-template <int QT, int MT_, int NT_> struct W32Geom {
-  static constexpr int NW = 4, MT = MT_, NT = NT_, BM = 32 * MT, BN = 32 * NT, SB = 4;
+template <int QT, int MT_, int NT_, int MH_> struct W32Geom {
+  // MH row halves of MT row tiles each; 4·MH waves: wave w takes K group w % 4 of row half w / 4
+  static constexpr int MH = MH_, NW = 4 * MH, MT = MT_, NT = NT_, BM = 32 * MT * MH, BN = 32 * NT, SB = 4;
   static constexpr int BB = QT == LK_TYPE_Q4_1 ? 20 : 18;
   static constexpr int WIN = 80;                            // bytes per row per stage (4 blocks: 72 / 80 B)
   static constexpr int WP = WIN / 16;                       // 16-B pieces per row
@@ -58,10 +66,10 @@ template <int QT, int MT_, int NT_> struct W32Geom {
   static constexpr int D = D0 > 5 ? 5 : D0;                 // ring slots (D − 2 stages in flight ahead)
   static constexpr int LDS = D * STAGE;
   static constexpr int OVERREAD = WIN - SB * BB;            // bytes a row's last window reads past it
-  static constexpr int CHAINS = MT * NT;
+  static constexpr int CHAINS = MT * NT;                    // per wave
   static_assert(STAGE >= PAD_OFF + 1024, "stage layout");
   static_assert(D >= 3 && (D - 2) * CW < 64, "ring");
-  static_assert(CHAINS * NW * 4096 <= LDS, "K-group reduction buffer ([chain][group] x 4 KB)");
+  static_assert(MH * CHAINS * 4 * 4096 <= LDS, "K-group reduction buffer ([half][chain][group] x 4 KB)");
   static_assert(4 * BN <= 1024, "T slot");
 };
 
@@ -74,6 +82,7 @@ struct XSplit32Args {
   float mult;            // −136 (Q4_0) or −128 (Q4_1)
 };
 
+#ifdef LK_W32_KERNELS  // the kernels live in their own translation unit (lk_w32.hip: MFMA results in VGPRs)
 // One wave per (32-column tile t, block kb); lane (n = lane & 31, h = lane >> 5) writes, for step s,
 // x(n, 32kb + 8(2h + s) + ord[j]) (ord = 0,4,1,5,2,6,3,7: q4_codes_128's element order of code dword
 // 2h + s) split into bf16 hi (truncated) and lo (x − hi rounded to nearest even), as fragment
@@ -154,12 +163,19 @@ __device__ __forceinline__ void w32_block(const u32x4 &p0, const u32x4 &p1, int 
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int QT, int MT, int NT, int G>
-__device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm, int tn, int st0, int st1,
+#ifdef LK_LAB_W32_STAMPS  // lab builds only (tools/stamp_w32.py): per-wave cycle counts of the main loop
+__device__ uint64_t lk_w32_stamps[1024][4][8];
+#define LK_W32_T() __builtin_amdgcn_s_memtime()
+#else
+#define LK_W32_T() 0ull
+#endif
+
+template <int QT, int MT, int NT, int MH, int G>
+__device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm, int tn, int st0, int st1, int wave, int mh,
                                          f32x16 (&acc)[MT][NT]) {
-  using W = W32Geom<QT, MT, NT>;
+  using W = W32Geom<QT, MT, NT, MH>;
   constexpr int D = W::D, CW = W::CW;
-  const int lane = threadIdx.x & 63, wave = G, h = lane >> 5, m = lane & 31;
+  const int lane = threadIdx.x & 63, h = lane >> 5, m = lane & 31;
   const int nblk = g.K / 32, ntx = (g.N + 31) / 32, n32 = ntx * 32;
   const int64_t RB = (int64_t)nblk * W::BB;
   const int nst = st1 - st0;
@@ -189,86 +205,146 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
       kind[c] = 3;
     }
   }
+  // the ring's LDS address as a number once (a generic -> LDS pointer cast per DMA costs a null check)
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LK_LDS const void *)smem);
+  // per-lane LDS read offsets inside a slot: this lane's row window at block G's pieces; fragment lane
+  // slot of block G; T of block G, rows 4h.. of a column tile
+  const uint32_t wofs_l = (uint32_t)((mh * MT * 32 + m) * W::WIN + G * 16), xofs_l = (uint32_t)(W::X_OFF + G * 4 * 1024 + lane * 16),
+                 tofs_l = (uint32_t)(W::T_OFF + (G * W::BN + 4 * h) * 4);
   auto issue = [&](int st, int sl) __attribute__((always_inline)) {
     const int kb = (st0 + min(st, nst - 1)) * W::SB;  // past the last stage: reload it (never read)
     const uint8_t *bw = g.a + (int64_t)kb * W::BB;
     const uint8_t *bx = (const uint8_t *)g.frag + (int64_t)kb * 4 * 1024;
     const uint8_t *bt = (const uint8_t *)(g.tsum + (int64_t)kb * n32);
-    uint8_t *slot = smem + sl * W::STAGE;
+    const uint32_t slot = lds0 + (uint32_t)(sl * W::STAGE);
 #pragma unroll
     for (int c = 0; c < CW; c++) {
       const int q = wave * CW + c;
       const uint8_t *base = kind[c] == 0 ? bw : kind[c] == 1 ? bx : bt;
-      uint8_t *to = kind[c] == 3 ? slot + W::PAD_OFF : slot + q * 1024;
-      dma16<false>(base, vofs[c], to);
+      dma16m(base, vofs[c], kind[c] == 3 ? slot + W::PAD_OFF : slot + q * 1024);
     }
   };
   // D − 1 stages in flight at the start; stage st's slot is refilled with stage st + D − 1 one stage later
 #pragma unroll
   for (int st = 0; st < D - 1; st++) issue(st, st);
+  [[maybe_unused]] uint64_t t_wait = 0, t_bar = 0, t0 = LK_W32_T();
   for (int st = 0; st < nst; st++) {
+    [[maybe_unused]] const uint64_t tw0 = LK_W32_T();
     wait_vmcnt<(D - 2) * CW>();    // this wave's DMAs of stage st have landed (D − 2 younger stages may not)
+#ifdef LK_LAB_W32_STAMPS
+    asm volatile("" ::: "memory");
+    const uint64_t tb = LK_W32_T();
+    t_wait += tb - tw0;
+#endif
     __builtin_amdgcn_s_barrier();  // ... every wave's; and every wave is done reading stage st − 1's slot
     asm volatile("" ::: "memory");
+#ifdef LK_LAB_W32_STAMPS
+    t_bar += LK_W32_T() - tb;
+#endif
     issue(st + D - 1, (st + D - 1) % D);  // refill the slot stage st − 1 used
-    const uint8_t *S = smem + (st % D) * W::STAGE;
-    // operands of block G: weights (two pieces per row tile), fragments, T
-    u32x4 wp[MT][2];
+    // LDS addresses: one per-lane base per operand kind for this slot, everything else an immediate offset
+    const uint32_t sb = lds0 + (uint32_t)((st % D) * W::STAGE);
+    const LK_LDS uint8_t *pw = (const LK_LDS uint8_t *)(uintptr_t)(sb + wofs_l);
+    const LK_LDS uint8_t *px = (const LK_LDS uint8_t *)(uintptr_t)(sb + xofs_l);
+    const LK_LDS uint8_t *pt = (const LK_LDS uint8_t *)(uintptr_t)(sb + tofs_l);
+    // block G's weights of every row tile, decoded first (the raw pieces die here)
+    bf16x8 w0[MT], w1[MT];
+    float d[MT], mq[MT];
 #pragma unroll
     for (int i = 0; i < MT; i++) {
-      const uint8_t *rp = S + (i * 32 + m) * W::WIN + G * 16;
-      wp[i][0] = *(const u32x4 *)rp;
-      wp[i][1] = *(const u32x4 *)(rp + 16);
+      const u32x4 a0 = *(const LK_LDS u32x4 *)(pw + i * 32 * W::WIN), a1 = *(const LK_LDS u32x4 *)(pw + i * 32 * W::WIN + 16);
+      uint32_t c0, c1;
+      float mn;
+      w32_block<QT, G>(a0, a1, h, c0, c1, d[i], mn);
+      w0[i] = q4_codes_128(c0);
+      w1[i] = q4_codes_128(c1);
+      mq[i] = mn * -0.0078125f;  // Q4_1: m·Σx = (−m/128)·T, exact
     }
-    bf16x8 xh[NT][2], xl[NT][2];
+    // chains c = j·MT + i, column tile major (one column tile's fragments and T live at a time),
+    // software-pipelined by hand: chain c's four MFMAs are issued before chain c − 1's scale FMAs, so the
+    // matrix pipe runs while the VALU scales
+    bf16x8 xh[2], xl[2];
+    f32x16 T;
+    auto load_x = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < NT; j++)
-#pragma unroll
-      for (int s = 0; s < 2; s++) {
-        const u32x4 *fp = (const u32x4 *)(S + W::X_OFF + ((((j * W::SB + G) * 2 + s) * 2) * 1024)) + lane;
-        xh[j][s] = __builtin_bit_cast(bf16x8, fp[0]);
-        xl[j][s] = __builtin_bit_cast(bf16x8, fp[64]);
+      for (int s2 = 0; s2 < 2; s2++) {
+        const LK_LDS uint8_t *f = px + (j * W::SB * 4 + s2 * 2) * 1024;
+        xh[s2] = __builtin_bit_cast(bf16x8, *(const LK_LDS u32x4 *)f);
+        xl[s2] = __builtin_bit_cast(bf16x8, *(const LK_LDS u32x4 *)(f + 1024));
       }
-    f32x16 T[NT];
-#pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const float *tp = (const float *)(S + W::T_OFF) + G * W::BN + 32 * j + 4 * h;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        const f32x4 v = *(const f32x4 *)(tp + 8 * q);
-        T[j][4 * q] = v.x; T[j][4 * q + 1] = v.y; T[j][4 * q + 2] = v.z; T[j][4 * q + 3] = v.w;
+        const f32x4 v = *(const LK_LDS f32x4 *)(pt + (32 * j + 8 * q) * 4);
+        T[4 * q] = v.x; T[4 * q + 1] = v.y; T[4 * q + 2] = v.z; T[4 * q + 3] = v.w;
+      }
+    };
+    auto chain = [&](int i) __attribute__((always_inline)) {
+      f32x16 p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[0], w0[i], T, 0, 0, 0);
+      p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[0], w0[i], p, 0, 0, 0);
+      p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[1], w1[i], p, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[1], w1[i], p, 0, 0, 0);
+    };
+    auto scale = [&](int i, int j, const f32x16 &p, const f32x16 &t) __attribute__((always_inline)) {
+#if LK_W32_PK
+      // packed: 8 v_pk_fma_f32 per chain instead of 16 v_fma (the kernel is VALU-issue bound)
+      const f2v dd = {d[i], d[i]};
+      [[maybe_unused]] const f2v mm = {mq[i], mq[i]};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        f2v a = {acc[i][j][r], acc[i][j][r + 1]};
+        if constexpr (QT == LK_TYPE_Q4_1) a = __builtin_elementwise_fma(mm, f2v{t[r], t[r + 1]}, a);
+        a = __builtin_elementwise_fma(dd, f2v{p[r], p[r + 1]}, a);
+        acc[i][j][r] = a.x;
+        acc[i][j][r + 1] = a.y;
+      }
+#else
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        if constexpr (QT == LK_TYPE_Q4_1) acc[i][j][r] = fmaf(mq[i], t[r], acc[i][j][r]);
+        acc[i][j][r] = fmaf(d[i], p[r], acc[i][j][r]);
+      }
+#endif
+    };
+    f32x16 pa, ta;
+    int pi = 0, pj = 0;
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      load_x(j);
+#pragma unroll
+      for (int i = 0; i < MT; i++) {
+        const f32x16 pb = chain(i);
+        if (j + i > 0) scale(pi, pj, pa, ta);
+        pa = pb;
+        ta = T;
+        pi = i;
+        pj = j;
       }
     }
+    scale(MT - 1, NT - 1, pa, ta);
+#if LK_W32_SCHED
+    // one MFMA, then its share of the VALU (decode + scale FMAs), so the VALU issues in the MFMAs' shadow
 #pragma unroll
-    for (int i = 0; i < MT; i++) {
-      uint32_t c0, c1;
-      float d, mn;
-      w32_block<QT, G>(wp[i][0], wp[i][1], h, c0, c1, d, mn);
-      const bf16x8 w0 = q4_codes_128(c0), w1 = q4_codes_128(c1);
-      [[maybe_unused]] const float mq = mn * -0.0078125f;  // Q4_1: m·Σx = (−m/128)·T, exact
-#pragma unroll
-      for (int j = 0; j < NT; j++) {
-        f32x16 p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[j][0], w0, T[j], 0, 0, 0);
-        p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[j][0], w0, p, 0, 0, 0);
-        p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[j][1], w1, p, 0, 0, 0);
-        p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[j][1], w1, p, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-          if constexpr (QT == LK_TYPE_Q4_1) acc[i][j][r] = fmaf(mq, T[j][r], acc[i][j][r]);
-          acc[i][j][r] = fmaf(d, p[r], acc[i][j][r]);
-        }
-      }
+    for (int q = 0; q < 4 * MT * NT; q++) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, LK_W32_SCHED, 0);
     }
+#endif
   }
   wait_vmcnt<0>();  // the padding stages, before the ring is reused for the reduction
+#ifdef LK_LAB_W32_STAMPS
+  if (lane == 0 && blockIdx.x < 1024 && mh == 0) {
+    uint64_t *o = lk_w32_stamps[blockIdx.x][G];
+    o[0] = t0; o[1] = LK_W32_T(); o[2] = t_wait; o[3] = t_bar; o[4] = (uint64_t)nst;
+  }
+#endif
 }
 
-template <int QT, int MT, int NT>
-__global__ __launch_bounds__(256, 1) void gemm_w32_kernel(W32Args g) {
-  using W = W32Geom<QT, MT, NT>;
+template <int QT, int MT, int NT, int MH>
+__global__ __launch_bounds__(256 * MH, MH) void gemm_w32_kernel(W32Args g) {
+  using W = W32Geom<QT, MT, NT, MH>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = threadIdx.x & 63, h = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), kg = wave & 3, mh = wave >> 2;
   // task order (speed only: dispatch is observed round-robin over the 8 XCDs): workgroup b runs task
   // (b % 8)·(grid / 8) + b / 8; tasks are column tile major, then row tile, then slice, so an XCD walks
   // the row tiles of one column tile (its activation fragments stay in the XCD's L2)
@@ -286,50 +362,46 @@ __global__ __launch_bounds__(256, 1) void gemm_w32_kernel(W32Args g) {
 #pragma unroll
       for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
   if (st1 > st0) {
-    switch (wave) {  // K group = wave: its block's offsets are compile-time constants
-      case 0: w32_main<QT, MT, NT, 0>(g, smem, tm, tn, st0, st1, acc); break;
-      case 1: w32_main<QT, MT, NT, 1>(g, smem, tm, tn, st0, st1, acc); break;
-      case 2: w32_main<QT, MT, NT, 2>(g, smem, tm, tn, st0, st1, acc); break;
-      default: w32_main<QT, MT, NT, 3>(g, smem, tm, tn, st0, st1, acc); break;
+    switch (kg) {  // K group: its block's offsets are compile-time constants
+      case 0: w32_main<QT, MT, NT, MH, 0>(g, smem, tm, tn, st0, st1, wave, mh, acc); break;
+      case 1: w32_main<QT, MT, NT, MH, 1>(g, smem, tm, tn, st0, st1, wave, mh, acc); break;
+      case 2: w32_main<QT, MT, NT, MH, 2>(g, smem, tm, tn, st0, st1, wave, mh, acc); break;
+      default: w32_main<QT, MT, NT, MH, 3>(g, smem, tm, tn, st0, st1, wave, mh, acc); break;
     }
   }
-  // K groups summed in group order: chain c = i·NT + j is finished by wave c % 4; every wave parks its
-  // other chains in LDS ([chain][group] x 4 KB, lane-major float4s)
+  // K groups summed in group order: chain c = i·NT + j of row half mh is finished by wave mh·4 + c % 4;
+  // every wave parks its chains in LDS ([half][chain][group] x 4 KB, lane-major float4s)
+  constexpr int CH = W::CHAINS;
   __syncthreads();
   f32x4 *red = (f32x4 *)smem;
 #pragma unroll
-  for (int i = 0; i < MT; i++)
+  for (int c = 0; c < CH; c++) {
+    f32x4 *o = red + ((mh * CH + c) * 4 + kg) * 256 + lane;
 #pragma unroll
-    for (int j = 0; j < NT; j++) {
-      if ((i * NT + j) % 4 == wave) continue;
-      f32x4 *o = red + ((i * NT + j) * 4 + wave) * 256 + lane;
-#pragma unroll
-      for (int q = 0; q < 4; q++) o[q * 64] = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-    }
+    for (int q = 0; q < 4; q++) o[q * 64] = f32x4{acc[c / NT][c % NT][4 * q], acc[c / NT][c % NT][4 * q + 1], acc[c / NT][c % NT][4 * q + 2], acc[c / NT][c % NT][4 * q + 3]};
+  }
   __syncthreads();
-  f32x4 sum[(W::CHAINS + 3) / 4][4];  // this wave's chains, summed over the K groups
+  constexpr int OWN = (CH + 3) / 4;  // chains finished per wave (at most)
+  f32x4 sum[OWN][4];
 #pragma unroll
-  for (int i = 0; i < MT; i++)
+  for (int oc = 0; oc < OWN; oc++) {
+    const int c = oc * 4 + kg;
+    if (c >= CH) break;
 #pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const int c = i * NT + j;
-      if (c % 4 != wave) continue;
+    for (int q = 0; q < 4; q++) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int gk = 0; gk < 4; gk++) {
-          const f32x4 p = gk == wave ? f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}
-                                     : red[(c * 4 + gk) * 256 + q * 64 + lane];
-          if (gk == 0) v = p;  // group 0 as is (0 + x would turn −0.0 into +0.0)
-          else { v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w; }
-        }
-        sum[c / 4][q] = v;
+      for (int gk = 0; gk < 4; gk++) {
+        const f32x4 p = red[((mh * CH + c) * 4 + gk) * 256 + q * 64 + lane];
+        if (gk == 0) v = p;  // group 0 as is (0 + x would turn −0.0 into +0.0)
+        else { v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w; }
       }
+      sum[oc][q] = v;
     }
+  }
   auto store_chain = [&](int c, const f32x4 (&s)[4]) __attribute__((always_inline)) {
     const int i = c / NT, j = c % NT;
-    const int64_t mrow = (int64_t)tm * W::BM + 32 * i + (lane & 31);
+    const int64_t mrow = (int64_t)tm * W::BM + 32 * (mh * MT + i) + (lane & 31);
     if (mrow >= g.M) return;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -347,7 +419,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w32_kernel(W32Args g) {
   };
   if (g.slices == 1) {
 #pragma unroll
-    for (int c = wave; c < W::CHAINS; c += 4) store_chain(c, sum[c / 4]);
+    for (int oc = 0; oc < OWN; oc++)
+      if (oc * 4 + kg < CH) store_chain(oc * 4 + kg, sum[oc]);
     return;
   }
   // split K: this slice's tile written through (sc1), every wave drained, one agent-scope arrival; the
@@ -357,29 +430,32 @@ __global__ __launch_bounds__(256, 1) void gemm_w32_kernel(W32Args g) {
   const int64_t slab = (int64_t)W::BM * W::BN;  // floats per tile
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc((void *)g.partial, 0, (int)((int64_t)g.slices * tiles * slab * 4), 0x00020000);
-  auto at = [&](int sl, int c, int q) __attribute__((always_inline)) {  // a lane's float4 of chain c
-    return (int)((((int64_t)sl * tiles + tile) * slab + ((int64_t)c * 4 + q) * 256 + 4 * lane) * 4);
+  auto at = [&](int sl, int c, int q) __attribute__((always_inline)) {  // a lane's float4 of chain c of half mh
+    return (int)((((int64_t)sl * tiles + tile) * slab + ((int64_t)(mh * CH + c) * 4 + q) * 256 + 4 * lane) * 4);
   };
 #pragma unroll
-  for (int c = wave; c < W::CHAINS; c += 4)
+  for (int oc = 0; oc < OWN; oc++)
+    if (oc * 4 + kg < CH)
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sum[c / 4][q]), prs, at(slice, c, q), 0, 16);
+      for (int q = 0; q < 4; q++)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sum[oc][q]), prs, at(slice, oc * 4 + kg, q), 0, 16);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int *flag = (int *)smem + 64 * 1024 / 4;  // past the reduction buffer's chains read above
+  int *flag = (int *)smem + 64 * 1024 / 4;  // inside the reduction buffer, every read of which is done
   if (threadIdx.x == 0) *flag = splitk_arrive(g.tcnt + (int64_t)tile * kChainLine, (unsigned)g.slices) ? 1 : 0;
   __syncthreads();
   asm volatile("" ::: "memory");
   if (!*flag) return;
 #pragma unroll
-  for (int c = wave; c < W::CHAINS; c += 4) {
+  for (int oc = 0; oc < OWN; oc++) {
+    const int c = oc * 4 + kg;
+    if (c >= CH) break;
     f32x4 t[4];
     for (int sl = 0; sl < g.slices; sl++) {
       f32x4 v[4];
 #pragma unroll
       for (int q = 0; q < 4; q++)
-        v[q] = sl == slice ? sum[c / 4][q] : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, at(sl, c, q), 0, 16));
+        v[q] = sl == slice ? sum[oc][q] : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, at(sl, c, q), 0, 16));
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         if (sl == 0) t[q] = v[q];
@@ -389,5 +465,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w32_kernel(W32Args g) {
     store_chain(c, t);
   }
 }
+
+#endif  // LK_W32_KERNELS
+
+// Launchers (lk_w32.hip): enqueue on `st`; hipGetLastError is the caller's.
+void w32_launch_xsplit(const XSplit32Args &xa, unsigned grid, hipStream_t st);
+void w32_launch(int qt, int mt, int nt, int mh, const W32Args &g, unsigned grid, size_t lds, hipStream_t st);
 
 }  // namespace lk
