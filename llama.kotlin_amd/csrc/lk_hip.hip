@@ -947,7 +947,11 @@ int launch_wide_t(WideArgs g, XSplitArgs xa, hipStream_t st) {
 // last row's last window (OVERREAD bytes past the matrix) inside A's buffer, 32-bit DMA and slab offsets.
 bool w32_eligible(const lk_tensor *a, const Checked &c) {
   static const bool off = getenv("LK_W32_OFF") != nullptr;  // A/B only: back to the round-5 kernels
-  if (off || (a->type != LK_TYPE_Q4_0 && a->type != LK_TYPE_Q4_1) || c.N <= 16 || c.K % 128) return false;
+  // N <= 32 stays on the skinny / pair / kpart kernels: the w32 shape for C3 (<Q, 3, 1, 1>, two K slices)
+  // measured 24.4-24.9 us against the pair kernel's 20.5-20.9 (A/B, two rounds);
+  // LK_W32_SKINNY=1 routes 17 <= N <= 32 here anyway (A/B only)
+  static const bool skinny = getenv("LK_W32_SKINNY") != nullptr;
+  if (off || (a->type != LK_TYPE_Q4_0 && a->type != LK_TYPE_Q4_1) || c.N <= (skinny ? 16 : 32) || c.K % 128) return false;
   const uintptr_t base = (uintptr_t)a->data + a->data_offset;
   const uint64_t bb = a->type == LK_TYPE_Q4_1 ? 20 : 18;
   const uint64_t over = a->type == LK_TYPE_Q4_1 ? W32Geom<LK_TYPE_Q4_1, 2, 2, 2>::OVERREAD : W32Geom<LK_TYPE_Q4_0, 2, 2, 2>::OVERREAD;

@@ -31,6 +31,12 @@
 #ifndef LK_W32_PK
 #define LK_W32_PK 1  // packed scale FMAs (lab: 0 = scalar)
 #endif
+#ifndef LK_W32_SPREAD
+#define LK_W32_SPREAD 0  // lab: 1 = half of a stage's DMAs issued before its last column tile's chains
+#endif
+#ifndef LK_W32_PRIO
+#define LK_W32_PRIO 1  // issue priority 1 for the second-dispatched row half (waves 4-7): 52.2-52.5 us vs 54.0 at C5 (lab: 0)
+#endif
 #ifndef LK_W32_SCHED
 #define LK_W32_SCHED 0  // lab: VALU instructions per MFMA enforced by sched_group_barrier (0: the compiler's order)
 #endif
@@ -211,14 +217,14 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
   // slot of block G; T of block G, rows 4h.. of a column tile
   const uint32_t wofs_l = (uint32_t)((mh * MT * 32 + m) * W::WIN + G * 16), xofs_l = (uint32_t)(W::X_OFF + G * 4 * 1024 + lane * 16),
                  tofs_l = (uint32_t)(W::T_OFF + (G * W::BN + 4 * h) * 4);
-  auto issue = [&](int st, int sl) __attribute__((always_inline)) {
+  auto issue = [&](int st, int sl, int c0 = 0, int c1 = W::CW) __attribute__((always_inline)) {
     const int kb = (st0 + min(st, nst - 1)) * W::SB;  // past the last stage: reload it (never read)
     const uint8_t *bw = g.a + (int64_t)kb * W::BB;
     const uint8_t *bx = (const uint8_t *)g.frag + (int64_t)kb * 4 * 1024;
     const uint8_t *bt = (const uint8_t *)(g.tsum + (int64_t)kb * n32);
     const uint32_t slot = lds0 + (uint32_t)(sl * W::STAGE);
 #pragma unroll
-    for (int c = 0; c < CW; c++) {
+    for (int c = c0; c < c1; c++) {
       const int q = wave * CW + c;
       const uint8_t *base = kind[c] == 0 ? bw : kind[c] == 1 ? bx : bt;
       dma16m(base, vofs[c], kind[c] == 3 ? slot + W::PAD_OFF : slot + q * 1024);
@@ -227,7 +233,7 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
   // D − 1 stages in flight at the start; stage st's slot is refilled with stage st + D − 1 one stage later
 #pragma unroll
   for (int st = 0; st < D - 1; st++) issue(st, st);
-  [[maybe_unused]] uint64_t t_wait = 0, t_bar = 0, t0 = LK_W32_T();
+  [[maybe_unused]] uint64_t t_wait = 0, t_bar = 0, t_iss = 0, t_rd = 0, t0 = LK_W32_T();
   for (int st = 0; st < nst; st++) {
     [[maybe_unused]] const uint64_t tw0 = LK_W32_T();
     wait_vmcnt<(D - 2) * CW>();    // this wave's DMAs of stage st have landed (D − 2 younger stages may not)
@@ -241,7 +247,19 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
 #ifdef LK_LAB_W32_STAMPS
     t_bar += LK_W32_T() - tb;
 #endif
+#ifdef LK_LAB_W32_STAMPS
+    const uint64_t ti0 = LK_W32_T();
+#endif
+#if LK_W32_SPREAD
+    issue(st + D - 1, (st + D - 1) % D, 0, (CW + 1) / 2);  // refill the slot stage st − 1 used: half now,
+#else
     issue(st + D - 1, (st + D - 1) % D);  // refill the slot stage st − 1 used
+#endif
+#ifdef LK_LAB_W32_STAMPS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t ti1 = LK_W32_T();
+    t_iss += ti1 - ti0;
+#endif
     // LDS addresses: one per-lane base per operand kind for this slot, everything else an immediate offset
     const uint32_t sb = lds0 + (uint32_t)((st % D) * W::STAGE);
     const LK_LDS uint8_t *pw = (const LK_LDS uint8_t *)(uintptr_t)(sb + wofs_l);
@@ -309,6 +327,9 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
     int pi = 0, pj = 0;
 #pragma unroll
     for (int j = 0; j < NT; j++) {
+#if LK_W32_SPREAD
+      if (j == NT - 1) issue(st + D - 1, (st + D - 1) % D, (CW + 1) / 2, CW);  // ... half with the last column tile
+#endif
       load_x(j);
 #pragma unroll
       for (int i = 0; i < MT; i++) {
@@ -334,7 +355,7 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
 #ifdef LK_LAB_W32_STAMPS
   if (lane == 0 && blockIdx.x < 1024 && mh == 0) {
     uint64_t *o = lk_w32_stamps[blockIdx.x][G];
-    o[0] = t0; o[1] = LK_W32_T(); o[2] = t_wait; o[3] = t_bar; o[4] = (uint64_t)nst;
+    o[0] = t0; o[1] = LK_W32_T(); o[2] = t_wait; o[3] = t_bar; o[4] = (uint64_t)nst; o[5] = t_iss;
   }
 #endif
 }
@@ -345,6 +366,9 @@ __global__ __launch_bounds__(256 * MH, MH) void gemm_w32_kernel(W32Args g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), kg = wave & 3, mh = wave >> 2;
+#if LK_W32_PRIO
+  if (mh) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half loses arbitration (MI355X_MICROARCH.md)
+#endif
   // task order (speed only: dispatch is observed round-robin over the 8 XCDs): workgroup b runs task
   // (b % 8)·(grid / 8) + b / 8; tasks are column tile major, then row tile, then slice, so an XCD walks
   // the row tiles of one column tile (its activation fragments stay in the XCD's L2)

@@ -64,11 +64,12 @@ ROUTES = [
     (2, 256, 384, 4, "gemm_q_"),        # 216-B rows: not skinny-eligible; 12 K slices, tile counters
                                         # (gemm_q_lds with slack past A's bytes, else gemm_q_mfma)
     (2, 4096, 4096, 8, "kpart"),        # two K slices added into dst
-    (2, 11008, 4096, 32, "w32<2,3,1>"), # C3 since round 6: two K slices, last arriver per tile (tcnt)
-    (3, 4096, 11008, 32, "w32<3,3,1>"), # Q4_1 down projection: five K slices
+    (2, 11008, 4096, 32, "pair"),       # eight slices, reduce launch
+    (3, 4096, 4096, 64, "w32<3,2,2,2>"), # Q4_1 at N > 32 (round 6): one slice per tile, no counters
+    (2, 512, 4096, 64, "w32<2,2,2,2>"), # few tiles: K split over workgroups, last arriver per tile (tcnt)
     (6, 4096, 4096, 8, "skinny"),       # Q8_0
     (6, 4096, 4096, 64, "wide"),        # Q8_0: last arriver per tile (tcnt)
-    (2, 4096, 4096, 64, "w32"),         # Q4_0 at N > 32: no split K since round 6
+
     (3, 96, 1184, 40, "gemm_q_mfma"),   # Q4_1, 37 blocks per row: neither wide- nor LDS-eligible
 ]
 

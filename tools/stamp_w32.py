@@ -44,12 +44,14 @@ def main():
         wait = st[:, :, 2][live]
         bar = st[:, :, 3][live]
         nst = st[:, :, 4][live]
+        iss = st[:, :, 5][live]
         out[name] = {"route": route, "waves": int(live.sum()), "stages_per_wave": float(np.median(nst)),
                      "loop_cycles_median": float(np.median(loop)), "loop_cycles_max": float(loop.max()),
                      "vmcnt_wait_median": float(np.median(wait)), "barrier_wait_median": float(np.median(bar)),
                      "per_stage_cycles": float(np.median(loop / np.maximum(nst, 1))),
                      "per_stage_wait": float(np.median(wait / np.maximum(nst, 1))),
-                     "per_stage_barrier": float(np.median(bar / np.maximum(nst, 1)))}
+                     "per_stage_barrier": float(np.median(bar / np.maximum(nst, 1))),
+                     "per_stage_dma_issue": float(np.median(iss / np.maximum(nst, 1)))}
         del g
     print(json.dumps(out))
 
