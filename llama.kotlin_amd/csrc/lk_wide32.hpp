@@ -250,7 +250,8 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
 #ifdef LK_LAB_W32_STAMPS
     const uint64_t ti0 = LK_W32_T();
 #endif
-#if LK_W32_SPREAD
+#if defined(LK_LAB_W32_NO_REFILL)  // skeleton (wrong results): the prologue's stages only
+#elif LK_W32_SPREAD
     issue(st + D - 1, (st + D - 1) % D, 0, (CW + 1) / 2);  // refill the slot stage st − 1 used: half now,
 #else
     issue(st + D - 1, (st + D - 1) % D);  // refill the slot stage st − 1 used
@@ -286,23 +287,43 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
     auto load_x = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; s2++) {
+#ifdef LK_LAB_W32_HALF_X  // skeleton (wrong results): every column tile reads tile 0's fragments
+        const LK_LDS uint8_t *f = px + (s2 * 2) * 1024;
+#else
         const LK_LDS uint8_t *f = px + (j * W::SB * 4 + s2 * 2) * 1024;
+#endif
         xh[s2] = __builtin_bit_cast(bf16x8, *(const LK_LDS u32x4 *)f);
         xl[s2] = __builtin_bit_cast(bf16x8, *(const LK_LDS u32x4 *)(f + 1024));
       }
+#ifdef LK_LAB_W32_NO_T  // skeleton (wrong results): no T reads
+#pragma unroll
+      for (int q = 0; q < 16; q++) T[q] = (float)(j + q);
+#else
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const f32x4 v = *(const LK_LDS f32x4 *)(pt + (32 * j + 8 * q) * 4);
         T[4 * q] = v.x; T[4 * q + 1] = v.y; T[4 * q + 2] = v.z; T[4 * q + 3] = v.w;
       }
+#endif
     };
-    auto chain = [&](int i) __attribute__((always_inline)) {
+    auto chain = [&](int i) __attribute__((always_inline)) -> f32x16 {
+#ifdef LK_LAB_W32_NO_MFMA  // skeleton (wrong results): operands consumed by one VALU op, no MFMA
+      f32x16 q = T;
+      q[0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, xl[0]).x ^ __builtin_bit_cast(u32x4, xh[0]).y ^
+                                            __builtin_bit_cast(u32x4, xl[1]).z ^ __builtin_bit_cast(u32x4, xh[1]).w ^
+                                            __builtin_bit_cast(u32x4, w0[i]).x ^ __builtin_bit_cast(u32x4, w1[i]).y);
+      return q;
+#endif
       f32x16 p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[0], w0[i], T, 0, 0, 0);
       p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[0], w0[i], p, 0, 0, 0);
       p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[1], w1[i], p, 0, 0, 0);
       return __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[1], w1[i], p, 0, 0, 0);
     };
     auto scale = [&](int i, int j, const f32x16 &p, const f32x16 &t) __attribute__((always_inline)) {
+#ifdef LK_LAB_W32_NO_SCALE  // skeleton (wrong results): one add per chain instead of the scale FMAs
+      acc[i][j][0] += p[0] + p[15] + d[i];
+      return;
+#endif
 #if LK_W32_PK
       // packed: 8 v_pk_fma_f32 per chain instead of 16 v_fma (the kernel is VALU-issue bound)
       const f2v dd = {d[i], d[i]};
