@@ -973,6 +973,12 @@ int launch_w32_t(W32Args g, hipStream_t st) {
   slices = (nst + g.sstages - 1) / g.sstages;
   g.slices = slices;
   g.tasks = tiles * slices;
+  // column tiles per task group: an XCD's run of tasks (about tasks / 8) covers a block of row tiles x
+  // bc column tiles (LK_W32_BC overrides; A/B only). C5, A/B three rounds on one box: bc = 1 / 2 / 4 / 8
+  // 52.0-52.1 / 51.9-52.3 / 52.7-53.1 / 53.3-53.5 us per call; FETCH_SIZE x 2 of the GEMM 86.6 MB at
+  // bc = 1, 53.6 MB at bc = 4
+  static const int bc_env = [] { const char *e = getenv("LK_W32_BC"); return e ? atoi(e) : 0; }();
+  g.bc = std::max(1, std::min(bc_env > 0 ? bc_env : 2, g.tiles_n));
   if (slices > 1) {
     GemmScratch &S = gemm_scratch(st);
     const size_t pb = (size_t)slices * tiles * W::BM * W::BN * sizeof(float);

@@ -52,6 +52,7 @@ struct W32Args {
   int32_t M, N, K;
   int32_t tiles_m, tiles_n, tasks;
   int32_t slices, sstages;   // split K: slice s covers stages [s·sstages, (s + 1)·sstages)
+  int32_t bc;                // column tiles per task group (see gemm_w32_kernel's task order)
   float *partial;            // [slices][tiles][BM·BN] (slices > 1), lane-major per chain
   unsigned *tcnt;            // per-tile arrival counters (kChainLine apart), zero between launches
 };
@@ -391,12 +392,17 @@ __global__ __launch_bounds__(256 * MH, MH) void gemm_w32_kernel(W32Args g) {
   if (mh) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half loses arbitration (MI355X_MICROARCH.md)
 #endif
   // task order (speed only: dispatch is observed round-robin over the 8 XCDs): workgroup b runs task
-  // (b % 8)·(grid / 8) + b / 8; tasks are column tile major, then row tile, then slice, so an XCD walks
-  // the row tiles of one column tile (its activation fragments stay in the XCD's L2)
+  // (b % 8)·(grid / 8) + b / 8, so each XCD takes a contiguous run of tasks. Tiles are ordered in groups
+  // of bc column tiles: group, then row tile, then column tile within the group, then slice — a run of
+  // tasks covers a block of row tiles x bc column tiles, whose weight windows and activation fragments
+  // the XCD's L2 serves to its CUs (bc = 1: a run walks the row tiles of one column tile and every XCD
+  // re-fetches all the weights; C5 FETCH_SIZE x 2 86.6 MB per dispatch)
   const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
   if (task >= g.tasks) return;  // grid padding
   const int slice = task % g.slices, tile = task / g.slices;
-  const int tn = tile / g.tiles_m, tm = tile % g.tiles_m;
+  const int grp = tile / (g.tiles_m * g.bc), rem = tile - grp * g.tiles_m * g.bc;
+  const int bcg = min(g.bc, g.tiles_n - grp * g.bc);  // the last group may be narrower
+  const int tm = rem / bcg, tn = grp * g.bc + rem % bcg;
   const int nst = g.K / 32 / W::SB;
   const int st0 = slice * g.sstages, st1 = min(st0 + g.sstages, nst);
   f32x16 acc[MT][NT];
