@@ -861,6 +861,11 @@ int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   g.dst = (uint8_t *)dst->data + dst->data_offset;
   g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
+  // the Q4_0 pair kernel's conflict-free LDS rows read up to 8 bytes past a row piece (SkinnyPairGeom::XC)
+  // (opt-in: 2.0 -> 0.2 bank-conflict cycles per LDS instruction, but C3 Q4_0 21.27 -> 21.69 us per call,
+  // A/B three rounds: the shifted rows touch one more line each)
+  static const bool shift = getenv_flag("LK_SKP_SHIFT");
+  g.shift8 = (shift && a->type == LK_TYPE_Q4_0 && c.a_hi + 8 <= a->buf_bytes) ? 8 : 0;
   // Q4_0 / Q4_1 at N <= 16 with at most two K slices (K <= 4096) on the K-partitioned kernel (round 4:
   // the slices add into dst); otherwise the skinny / pair kernels with the slab reduce launch
   // (measured round 4: N = 8 / 16 16.2 / 16.4 vs 17.5 / 17.7 µs; C3 N = 32 23.3 vs 23.0; the down

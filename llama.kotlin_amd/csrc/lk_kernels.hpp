@@ -619,6 +619,7 @@ __device__ __forceinline__ void gemv_stream_body(const StreamWork *__restrict__ 
         const int p = min(i >> 4, NP - 1), t = (i & 15) ^ ((i >> 4) & 15);
         // sc1 (aux 16) loads: another workgroup's write-through outputs; a multi-GPU rank loads at
         // system scope (sc0 sc1, aux 17): some of those rows were stored by peers
+        // (device-scope loads after the acquire measured the same: the chain's cost is the fences)
         xv[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (p * 16 + t) * 16, 0, PEER ? 17 : 16));
       }
     };
@@ -1563,6 +1564,9 @@ struct SkinnyArgs {
   // per `slices` value so every counter stays a multiple of slices between calls; the word after
   // the row's last counter is the timeout flag
   unsigned *rsync;
+  // gemm_skinny_pair_kernel, Q4_0: 8 when A's buffer holds 8 bytes past the last row, so rows 8-15 of a
+  // unit may be staged 8 bytes later in their LDS rows (bank-conflict-free weight reads); else 0
+  int32_t shift8;
 };
 
 // s_waitcnt vmcnt(BASE + j·STEP) for a run-time j in [0, J].
@@ -2022,9 +2026,13 @@ template <int QT, int NT> struct SkinnyPairGeom {
   static constexpr int SB = 16, SBH = 8;                // blocks per slice / per half
   static constexpr int RPH = SBH * BB;                  // bytes of a half row piece (multiple of 16)
   static constexpr int PPH = RPH / 16;                  // 16-B cells per half row
-  // cells per LDS row: odd, so the 16 rows of a unit start on 16 distinct 4-bank groups (Q4_1's
-  // 10 cells would put rows m and m + 8 on the same banks: 2-way conflicts on every weight read)
-  static constexpr int CPR = PPH | 1;
+  // cells per LDS row: odd, so rows m and m + 8 of a unit do not start on the same 4-bank group (Q4_1's
+  // 10 cells put them on the same banks: 2-way conflicts on every weight read). A 16-B cell pitch still
+  // maps rows m and m + 8 to one bank group of a 32-lane half (4·CPR·8 ≡ 0 mod 32), so Q4_0 (round 6)
+  // stages rows 8-15 8 bytes later (their DMA starts 8 bytes early, one more cell): the two rows' reads
+  // land on dwords {0, 1} and {2, 3} of a group — conflict-free — at the same 3 DMA instructions
+  static constexpr int XC = QT == LK_TYPE_Q4_0 ? 1 : 0;
+  static constexpr int CPR = (PPH + XC) | 1;
   static constexpr int PITCH = CPR * 16;                // LDS row pitch
   static constexpr int L = (16 * CPR + 63) / 64;        // DMA instructions per half unit
   static constexpr int WPB = QT == LK_TYPE_Q4_1 ? 2 : QT == LK_TYPE_Q4_0 ? 3 : 4;
@@ -2144,17 +2152,22 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   const int nunits = t1 - t0 - p > 0 ? (t1 - t0 - p + 3) / 4 : 0;  // stream p: tiles t0 + p + 4i
   const int pph = nbh * BB / 16;
   const int myL = nbh > 0 ? L : 0;
+  // Q4_0: rows 8-15 of a unit 8 bytes later in their LDS rows (SkinnyPairGeom::XC); reads follow
+  const int sh8 = QT == LK_TYPE_Q4_0 ? g.shift8 : 0;
+  const int rsh = (lane & 15) >= 8 ? sh8 : 0;
 
   // half unit u = rows of tile t0 + p + 4u, bytes [kb0·BB + h·RPH, + nbh·BB) of each; cell
   // q = r·CPR + c lands at slot + 16q (row pitch PITCH); pad cells and cells past the unit re-read cell 0
   const uint8_t *abase = g.a + (int64_t)kb0 * BB + (int64_t)h * G::RPH;
-  uint32_t rofs[L];
+  uint32_t rofs[L], dsh[L];
   int rrow[L];
 #pragma unroll
   for (int j = 0; j < L; j++) {
     const int q = j * 64 + lane, r = q / G::CPR, c = q % G::CPR;
+    const int shifted = r >= 8 && r < 16 && sh8;
     rrow[j] = min(r, 15);
-    rofs[j] = (uint32_t)((c < pph && r < 16) ? c * 16 : 0);
+    rofs[j] = (uint32_t)((c < pph + shifted && r < 16) ? c * 16 : 0);
+    dsh[j] = shifted ? 8u : 0u;
   }
   auto issue = [&](int u, int sl) __attribute__((always_inline)) {
     const int t = t0 + p + u * 4;
@@ -2162,7 +2175,10 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
     const int rmax = g.M - 1 - t * 16;
 #pragma unroll
     for (int j = 0; j < L; j++) {
-      const uint32_t vofs = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
+      // a shifted row starts 8 bytes early; a row clamped onto the matrix's first piece (its outputs
+      // are never stored) reads unshifted rather than before the tile's base
+      const uint32_t at = (uint32_t)(min(rrow[j], rmax) * RB) + rofs[j];
+      const uint32_t vofs = at >= dsh[j] ? at - dsh[j] : at;
       dma16<1>(tb, vofs, ring + sl * G::SLOT + j * 1024);  // nt: read once per launch
     }
   };
@@ -2274,7 +2290,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
       uint32_t wd[8][G::WPB];
       const uint8_t *slot_ptr = ring + slot * G::SLOT;
       {
-        const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::PITCH;
+        const uint8_t *bm = ring + slot * G::SLOT + (lane & 15) * G::PITCH + rsh;
         const uint8_t *bg = bm + (QT == LK_TYPE_Q8_0 ? 8 : 4) * (lane >> 4);
         skinny_read_all<QT, 8, G::WPB, 0>(bm, bg, wd);
         asm volatile("" ::: "memory");
@@ -2285,7 +2301,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
         // acc += Σ_b e_b(row)·T_b(column) over the half's 8 blocks, two f32 MFMAs (K = 4 blocks)
         // per 16-column tile: e = d (Q4_0, T = −136·Σ(hi + lo)) or m (Q4_1, T = Σx); lane
         // (m = lane & 15, b' = lane >> 4) reads its row's header of block 4c + b'
-        const uint8_t *hrow = slot_ptr + (lane & 15) * G::PITCH;
+        const uint8_t *hrow = slot_ptr + (lane & 15) * G::PITCH + rsh;
 #pragma unroll
         for (int c = 0; c < 2; c++) {
           const int bl = 4 * c + (lane >> 4);
