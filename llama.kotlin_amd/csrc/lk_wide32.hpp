@@ -37,6 +37,9 @@
 #ifndef LK_W32_PRIO
 #define LK_W32_PRIO 1  // issue priority 1 for the second-dispatched row half (waves 4-7): 52.2-52.5 us vs 54.0 at C5 (lab: 0)
 #endif
+#ifndef LK_W32_PP
+#define LK_W32_PP 0  // lab: 1 = the two row halves in ping-pong (w32_main_pp): C5 53.8-54.0 vs 52.3-52.6 us, not kept
+#endif
 #ifndef LK_W32_SCHED
 #define LK_W32_SCHED 0  // lab: VALU instructions per MFMA enforced by sched_group_barrier (0: the compiler's order)
 #endif
@@ -171,7 +174,7 @@ __device__ __forceinline__ void w32_block(const u32x4 &p0, const u32x4 &p1, int 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #ifdef LK_LAB_W32_STAMPS  // lab builds only (tools/stamp_w32.py): per-wave cycle counts of the main loop
-__device__ uint64_t lk_w32_stamps[1024][4][8];
+__device__ uint64_t lk_w32_stamps[1024][8][8];  // [workgroup][wave][slot]
 #define LK_W32_T() __builtin_amdgcn_s_memtime()
 #else
 #define LK_W32_T() 0ull
@@ -375,11 +378,202 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
   }
   wait_vmcnt<0>();  // the padding stages, before the ring is reused for the reduction
 #ifdef LK_LAB_W32_STAMPS
-  if (lane == 0 && blockIdx.x < 1024 && mh == 0) {
-    uint64_t *o = lk_w32_stamps[blockIdx.x][G];
+  if (lane == 0 && blockIdx.x < 1024) {
+    uint64_t *o = lk_w32_stamps[blockIdx.x][wave];
     o[0] = t0; o[1] = LK_W32_T(); o[2] = t_wait; o[3] = t_bar; o[4] = (uint64_t)nst; o[5] = t_iss;
   }
 #endif
+}
+
+// Two row halves in ping-pong (MH = 2, round 6): each SIMD holds one wave of each half, and the halves
+// alternate between an operand phase (the stage's LDS reads and code decode into registers) and a matrix
+// phase (the stage's MFMAs and scale FMAs from those registers), two workgroup barriers per stage. While
+// one half's wave reads LDS and decodes, the other half's wave on the same SIMD has the matrix pipe to
+// itself, instead of both reading, then both queueing for the MFMAs, then both waiting at one barrier.
+//   even barrier (stage st): half 0 reads stage st; half 1 multiplies stage st − 1
+//   odd barrier:             half 0 multiplies stage st; half 1 reads stage st
+// Stage st's slot is read in the even interval (half 0) and the odd one (half 1), so the refill issued
+// after the next even barrier may overwrite it; a half waits for its own LDS reads before that barrier.
+template <int QT, int MT, int NT, int MH, int G>
+__device__ __forceinline__ void w32_main_pp(const W32Args &g, uint8_t *smem, int tm, int tn, int st0, int st1, int wave, int mh,
+                                            f32x16 (&acc)[MT][NT]) {
+  using W = W32Geom<QT, MT, NT, MH>;
+  constexpr int D = W::D, CW = W::CW;
+  const int lane = threadIdx.x & 63, h = lane >> 5, m = lane & 31;
+  const int nblk = g.K / 32, ntx = (g.N + 31) / 32, n32 = ntx * 32;
+  const int64_t RB = (int64_t)nblk * W::BB;
+  const int nst = st1 - st0;
+  uint32_t vofs[CW];
+  int kind[CW];  // 0 weights, 1 fragments, 2 T, 3 padding (wave-uniform)
+#pragma unroll
+  for (int c = 0; c < CW; c++) {
+    const int q = wave * CW + c;
+    if (q < W::W_INST) {
+      const int p = min(q * 64 + lane, W::BM * W::WP - 1), r = p / W::WP, pc = p % W::WP;
+      const int64_t row = min((int64_t)tm * W::BM + r, (int64_t)g.M - 1);
+      vofs[c] = (uint32_t)(row * RB + pc * 16);
+      kind[c] = 0;
+    } else if (q < W::W_INST + W::X_INST) {
+      const int f = q - W::W_INST, j = f / (W::SB * 4), b = (f / 4) % W::SB, s = (f / 2) % 2, sp = f % 2;
+      const int64_t xt = min(tn * NT + j, ntx - 1);
+      vofs[c] = (uint32_t)(((((xt * nblk + b) * 2 + s) * 2 + sp) * 64 + lane) * 16);
+      kind[c] = 1;
+    } else if (q == W::W_INST + W::X_INST) {
+      const int b = min(lane / (W::BN / 4), W::SB - 1), c4 = lane % (W::BN / 4);
+      const int col = min(tn * W::BN + 4 * c4, n32 - 4);
+      vofs[c] = (uint32_t)(((int64_t)b * n32 + col) * 4);
+      kind[c] = 2;
+    } else {
+      vofs[c] = 0;
+      kind[c] = 3;
+    }
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LK_LDS const void *)smem);
+  const uint32_t wofs_l = (uint32_t)((mh * MT * 32 + m) * W::WIN + G * 16), xofs_l = (uint32_t)(W::X_OFF + G * 4 * 1024 + lane * 16),
+                 tofs_l = (uint32_t)(W::T_OFF + (G * W::BN + 4 * h) * 4);
+  auto issue = [&](int st, int sl) __attribute__((always_inline)) {
+    const int kb = (st0 + min(st, nst - 1)) * W::SB;  // past the last stage: reload it (never read)
+    const uint8_t *bw = g.a + (int64_t)kb * W::BB;
+    const uint8_t *bx = (const uint8_t *)g.frag + (int64_t)kb * 4 * 1024;
+    const uint8_t *bt = (const uint8_t *)(g.tsum + (int64_t)kb * n32);
+    const uint32_t slot = lds0 + (uint32_t)(sl * W::STAGE);
+#pragma unroll
+    for (int c = 0; c < CW; c++) {
+      const int q = wave * CW + c;
+      const uint8_t *base = kind[c] == 0 ? bw : kind[c] == 1 ? bx : bt;
+      dma16m(base, vofs[c], kind[c] == 3 ? slot + W::PAD_OFF : slot + q * 1024);
+    }
+  };
+  // the operands of one stage, held from the operand phase to the matrix phase
+  bf16x8 w0[MT], w1[MT], xh[NT][2], xl[NT][2];
+  float d[MT], mq[MT];
+  f32x16 T[NT];
+  auto operands = [&](int st) __attribute__((always_inline)) {
+    const uint32_t sb = lds0 + (uint32_t)((st % D) * W::STAGE);
+    const LK_LDS uint8_t *pw = (const LK_LDS uint8_t *)(uintptr_t)(sb + wofs_l);
+    const LK_LDS uint8_t *px = (const LK_LDS uint8_t *)(uintptr_t)(sb + xofs_l);
+    const LK_LDS uint8_t *pt = (const LK_LDS uint8_t *)(uintptr_t)(sb + tofs_l);
+#pragma unroll
+    for (int i = 0; i < MT; i++) {
+      const u32x4 a0 = *(const LK_LDS u32x4 *)(pw + i * 32 * W::WIN), a1 = *(const LK_LDS u32x4 *)(pw + i * 32 * W::WIN + 16);
+      uint32_t c0, c1;
+      float mn;
+      w32_block<QT, G>(a0, a1, h, c0, c1, d[i], mn);
+      w0[i] = q4_codes_128(c0);
+      w1[i] = q4_codes_128(c1);
+      mq[i] = mn * -0.0078125f;  // Q4_1: m·Σx = (−m/128)·T, exact
+    }
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; s2++) {
+        const LK_LDS uint8_t *f = px + (j * W::SB * 4 + s2 * 2) * 1024;
+        xh[j][s2] = __builtin_bit_cast(bf16x8, *(const LK_LDS u32x4 *)f);
+        xl[j][s2] = __builtin_bit_cast(bf16x8, *(const LK_LDS u32x4 *)(f + 1024));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const f32x4 v = *(const LK_LDS f32x4 *)(pt + (32 * j + 8 * q) * 4);
+        T[j][4 * q] = v.x; T[j][4 * q + 1] = v.y; T[j][4 * q + 2] = v.z; T[j][4 * q + 3] = v.w;
+      }
+    }
+    wait_lgkmcnt0();  // this half's reads of the slot are done before the barrier that may refill it
+  };
+  auto matrix = [&]() __attribute__((always_inline)) {
+    auto chain = [&](int i, int j) __attribute__((always_inline)) -> f32x16 {
+      f32x16 p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[j][0], w0[i], T[j], 0, 0, 0);
+      p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[j][0], w0[i], p, 0, 0, 0);
+      p = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[j][1], w1[i], p, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[j][1], w1[i], p, 0, 0, 0);
+    };
+    auto scale = [&](int i, int j, const f32x16 &p) __attribute__((always_inline)) {
+      const f2v dd = {d[i], d[i]};
+      [[maybe_unused]] const f2v mm = {mq[i], mq[i]};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        f2v a = {acc[i][j][r], acc[i][j][r + 1]};
+        if constexpr (QT == LK_TYPE_Q4_1) a = __builtin_elementwise_fma(mm, f2v{T[j][r], T[j][r + 1]}, a);
+        a = __builtin_elementwise_fma(dd, f2v{p[r], p[r + 1]}, a);
+        acc[i][j][r] = a.x;
+        acc[i][j][r + 1] = a.y;
+      }
+    };
+    // chain c's MFMAs issued before chain c − 1's scale FMAs (hand pipelining, as w32_main)
+    f32x16 pa;
+    int pi = 0, pj = 0;
+#pragma unroll
+    for (int j = 0; j < NT; j++)
+#pragma unroll
+      for (int i = 0; i < MT; i++) {
+        const f32x16 pb = chain(i, j);
+        if (j + i > 0) scale(pi, pj, pa);
+        pa = pb;
+        pi = i;
+        pj = j;
+      }
+    scale(MT - 1, NT - 1, pa);
+  };
+#pragma unroll
+  for (int st = 0; st < D - 1; st++) issue(st, st);
+  // one loop per half (the same barrier count), so each keeps its operands in place across iterations
+  [[maybe_unused]] uint64_t t_op = 0, t_mx = 0, t_bar = 0, t_iss = 0, t0 = LK_W32_T(), ta;
+#ifdef LK_LAB_W32_STAMPS
+#define LK_PP_ACC(v) do { asm volatile("" ::: "memory"); const uint64_t tb_ = LK_W32_T(); v += tb_ - ta; ta = tb_; } while (0)
+#define LK_PP_MX() do { asm volatile("s_nop 0" ::: "memory"); } while (0)
+#else
+#define LK_PP_ACC(v) do { } while (0)
+#define LK_PP_MX() do { } while (0)
+#endif
+  ta = t0;
+  if (mh == 0) {
+    for (int st = 0; st < nst; st++) {
+      wait_vmcnt<(D - 2) * CW>();  // this wave's DMAs of stage st have landed
+      __builtin_amdgcn_s_barrier();  // ... every wave's; both halves are done with stage st − 1's slot
+      asm volatile("" ::: "memory");
+      LK_PP_ACC(t_bar);
+      issue(st + D - 1, (st + D - 1) % D);
+      LK_PP_ACC(t_iss);
+      operands(st);
+      LK_PP_ACC(t_op);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      LK_PP_ACC(t_bar);
+      matrix();  // stage st
+#ifdef LK_LAB_W32_STAMPS
+      { float z = 0.f; for (int i = 0; i < MT; i++) for (int j = 0; j < NT; j++) z += acc[i][j][0]; asm volatile("" :: "v"(z)); }
+#endif
+      LK_PP_ACC(t_mx);
+    }
+  } else {
+    for (int st = 0; st < nst; st++) {
+      wait_vmcnt<(D - 2) * CW>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      LK_PP_ACC(t_bar);
+      issue(st + D - 1, (st + D - 1) % D);
+      LK_PP_ACC(t_iss);
+      if (st > 0) matrix();  // stage st − 1
+#ifdef LK_LAB_W32_STAMPS
+      { float z = 0.f; for (int i = 0; i < MT; i++) for (int j = 0; j < NT; j++) z += acc[i][j][0]; asm volatile("" :: "v"(z)); }
+#endif
+      LK_PP_ACC(t_mx);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      LK_PP_ACC(t_bar);
+      operands(st);
+      LK_PP_ACC(t_op);
+    }
+    if (nst > 0) matrix();  // the last stage
+  }
+#undef LK_PP_ACC
+#undef LK_PP_MX
+  wait_vmcnt<0>();
+#ifdef LK_LAB_W32_STAMPS
+  if (lane == 0 && blockIdx.x < 1024) {
+    uint64_t *o = lk_w32_stamps[blockIdx.x][wave];
+    o[0] = t0; o[1] = LK_W32_T(); o[2] = t_op; o[3] = t_bar; o[4] = (uint64_t)nst; o[5] = t_iss; o[6] = t_mx;
+  }
+#endif  // the padding stages, before the ring is reused for the reduction
 }
 
 template <int QT, int MT, int NT, int MH>
@@ -414,10 +608,14 @@ __global__ __launch_bounds__(256 * MH, MH) void gemm_w32_kernel(W32Args g) {
       for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
   if (st1 > st0) {
     switch (kg) {  // K group: its block's offsets are compile-time constants
-      case 0: w32_main<QT, MT, NT, MH, 0>(g, smem, tm, tn, st0, st1, wave, mh, acc); break;
-      case 1: w32_main<QT, MT, NT, MH, 1>(g, smem, tm, tn, st0, st1, wave, mh, acc); break;
-      case 2: w32_main<QT, MT, NT, MH, 2>(g, smem, tm, tn, st0, st1, wave, mh, acc); break;
-      default: w32_main<QT, MT, NT, MH, 3>(g, smem, tm, tn, st0, st1, wave, mh, acc); break;
+#define LK_W32_MAIN(GG)                                                                   \
+  if constexpr (MH == 2 && LK_W32_PP) w32_main_pp<QT, MT, NT, MH, GG>(g, smem, tm, tn, st0, st1, wave, mh, acc); \
+  else w32_main<QT, MT, NT, MH, GG>(g, smem, tm, tn, st0, st1, wave, mh, acc);
+      case 0: LK_W32_MAIN(0) break;
+      case 1: LK_W32_MAIN(1) break;
+      case 2: LK_W32_MAIN(2) break;
+      default: LK_W32_MAIN(3) break;
+#undef LK_W32_MAIN
     }
   }
   // K groups summed in group order: chain c = i·NT + j of row half mh is finished by wave mh·4 + c % 4;

@@ -19,7 +19,7 @@ def main():
     dev = torch.device("cuda", 0)
     G.load_library()
     lib = ctypes.CDLL(os.environ["LK_HIP_LIB"])
-    buf = (ctypes.c_uint64 * (1024 * 4 * 8))()
+    buf = (ctypes.c_uint64 * (1024 * 8 * 8))()
     T = G.GGMLType
     s = torch.cuda.Stream(device=dev)
     out = {}
@@ -38,20 +38,21 @@ def main():
         s.synchronize()
         route = G.debugRoute()
         assert lib.lk_lab_w32_stamps(buf, len(buf)) == 0
-        st = np.frombuffer(buf, np.uint64).reshape(1024, 4, 8).astype(np.int64)
-        live = st[:, :, 4] > 0
-        loop = (st[:, :, 1] - st[:, :, 0])[live]
-        wait = st[:, :, 2][live]
-        bar = st[:, :, 3][live]
-        nst = st[:, :, 4][live]
-        iss = st[:, :, 5][live]
-        out[name] = {"route": route, "waves": int(live.sum()), "stages_per_wave": float(np.median(nst)),
-                     "loop_cycles_median": float(np.median(loop)), "loop_cycles_max": float(loop.max()),
-                     "vmcnt_wait_median": float(np.median(wait)), "barrier_wait_median": float(np.median(bar)),
-                     "per_stage_cycles": float(np.median(loop / np.maximum(nst, 1))),
-                     "per_stage_wait": float(np.median(wait / np.maximum(nst, 1))),
-                     "per_stage_barrier": float(np.median(bar / np.maximum(nst, 1))),
-                     "per_stage_dma_issue": float(np.median(iss / np.maximum(nst, 1)))}
+        st = np.frombuffer(buf, np.uint64).reshape(1024, 8, 8).astype(np.int64)
+        res = {"route": route}
+        # slots: w32_main 2 vmcnt wait, 3 barrier, 5 DMA issue; w32_main_pp 2 operand phase, 3 waits + barriers,
+        # 5 DMA issue, 6 matrix phase (cycles per stage, medians over waves of each row half)
+        for half, ws in (("half0", slice(0, 4)), ("half1", slice(4, 8))):
+            sub = st[:, ws, :]
+            live = sub[:, :, 4] > 0
+            if not live.any():
+                continue
+            nst = np.maximum(sub[:, :, 4][live], 1)
+            per = lambda k: float(np.median(sub[:, :, k][live] / nst))  # noqa: E731
+            res[half] = {"waves": int(live.sum()), "stages": float(np.median(nst)),
+                         "loop_per_stage": float(np.median((sub[:, :, 1] - sub[:, :, 0])[live] / nst)),
+                         "slot2": per(2), "slot3": per(3), "slot5_issue": per(5), "slot6": per(6)}
+        out[name] = res
         del g
     print(json.dumps(out))
 
