@@ -681,31 +681,43 @@ int launch_skinny_t(SkinnyArgs g, hipStream_t st) {
   return LK_OK;
 }
 
+bool getenv_flag(const char *name);
+
+// gemm_skinny_pair_kernel's split-K tasks for g's shape: slices of SB blocks, row ranges filling the
+// CUs; returns the slab bytes (0 for one slice). Shared by the single launch and a plan's grouped launch,
+// so both compute the same bits.
+template <int QT, int NT>
+size_t pair_geometry(SkinnyArgs &g) {
+  using SG = SkinnyPairGeom<QT, NT>;
+  const int nblk = g.K / 32;
+  const int slices = (nblk + SG::SB - 1) / SG::SB;
+  const int ntile = (g.M + 15) / 16;
+  int ranges = std::max(1, std::min(ntile, cu_count() / slices));
+  g.tiles_per_range = (ntile + ranges - 1) / ranges;
+  ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
+  g.slices = slices;
+  g.tasks = ranges * slices;
+  return slices > 1 ? (size_t)slices * g.M * 16 * NT * sizeof(float) : 0;
+}
+
 // gemm_skinny_pair_kernel: the same split-K tasks, a wave pair per stream (8 waves).
 template <int QT, int NT>
 int launch_skinny_pair_t(SkinnyArgs g, hipStream_t st) {
   using SG = SkinnyPairGeom<QT, NT>;
   GemmScratch &S = gemm_scratch(st);
-  const int nblk = g.K / 32;
-  const int slices = (nblk + SG::SB - 1) / SG::SB;
-  const int ntile = (g.M + 15) / 16;
+  (void)pair_geometry<QT, NT>(g);
+  const int slices = g.slices, ntile = (g.M + 15) / 16, ranges = g.tasks / g.slices;
   // split-K fixed up by the last arriver per tile unless LK_SKP_UNFUSED=1 (splitk_counters)
-  const int cu = cu_count();
   const size_t slab_bytes = (size_t)slices * g.M * 16 * NT * sizeof(float);
-  int ranges = std::max(1, std::min(ntile, cu / slices));
-  g.tiles_per_range = (ntile + ranges - 1) / ranges;
-  ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   unsigned *rsync = nullptr;
   const bool list_ok = 1 + (g.tiles_per_range + 3) / 4 <= NT * 64 * 4;  // parity 0 of a pair's hand-off
   if (int rc = splitk_counters(slices, slab_bytes, ntile, list_ok, false, st, &rsync)) return rc;
   const bool fuse = rsync != nullptr;
-  g.slices = slices;
   if (slices > 1) {
     const int rc = grow(S, &S.partial, &S.partial_bytes, slab_bytes);
     if (rc) return rc;
     g.partial = (float *)S.partial;
   }
-  g.tasks = ranges * slices;
   g.rsync = rsync;
   const unsigned grid = (unsigned)((g.tasks + 7) / 8 * 8);
   note_route("pair<%d,%d>:s%dr%d%s", QT, NT, slices, ranges, fuse ? "f" : "");
@@ -773,6 +785,91 @@ int launch_sk_t(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Ch
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const float *)g.partial,
                        slices, g.M, g.N, 16 * NT, g.dst, g.d_nb0, g.d_nb1);
   }
+  HIP_TRY(hipGetLastError());
+  return LK_OK;
+}
+
+// ---- a plan's grouped pair-kernel launch (round 6) ----------------------------------------------
+// Independent 17 <= N <= 32 Q4 nodes of one type: one gemm_skinny_pair_group_kernel launch over all of
+// them and one splitk_reduce_group_kernel launch of their slab sums, with the SkinnyArgs each node's
+// single launch would use (pair_geometry: the same tasks, slices and summation order, so the same bits).
+// The slabs are owned by the plan (one plan must not run on two streams at once).
+struct PairNodeOps { const lk_tensor *a, *b, *d; const Checked *c; };
+struct PairGroupLaunch { int32_t qt = 0; int nn = 0, nred = 0; unsigned grid = 0, rgrid = 0; SkinnyArgs *nodes = nullptr;
+                         ReduceNode *red = nullptr; void *slabs = nullptr; };
+SkinnyArgs skinny_args(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const Checked &c);
+
+void free_pair_group(PairGroupLaunch &pg) {
+  if (pg.nodes) (void)hipFree(pg.nodes);
+  if (pg.red) (void)hipFree(pg.red);
+  if (pg.slabs) (void)hipFree(pg.slabs);
+  pg.nodes = nullptr; pg.red = nullptr; pg.slabs = nullptr;
+}
+
+int build_pair_group(int32_t qt, const std::vector<PairNodeOps> &ops, PairGroupLaunch &pg) {
+  std::vector<SkinnyArgs> nodes;
+  std::vector<ReduceNode> red;
+  std::vector<size_t> slab_off;
+  size_t slab_total = 0;
+  int64_t tasks = 0, rthreads = 0;
+  // heaviest tasks first (rows per task x blocks per slice): the dispatcher hands the light ones to the
+  // CUs that finish early (largest-first list scheduling); a node's bits do not depend on the order
+  std::vector<PairNodeOps> ord(ops);
+  auto cost = [](const PairNodeOps &o) {
+    SkinnyArgs g = skinny_args(o.a, o.b, o.d, *o.c);
+    (void)pair_geometry<LK_TYPE_Q4_0, 2>(g);
+    return (double)g.tiles_per_range * (double)std::min<int64_t>(16, o.c->K / 32);
+  };
+  std::stable_sort(ord.begin(), ord.end(), [&](const PairNodeOps &x, const PairNodeOps &y) { return cost(x) > cost(y); });
+  for (const auto &o : ord) {
+    SkinnyArgs g = skinny_args(o.a, o.b, o.d, *o.c);
+    const size_t sb = qt == LK_TYPE_Q4_0 ? pair_geometry<LK_TYPE_Q4_0, 2>(g) : pair_geometry<LK_TYPE_Q4_1, 2>(g);
+    slab_off.push_back(slab_total);
+    slab_total += (sb + 255) / 256 * 256;
+    tasks += g.tasks;
+    nodes.push_back(g);
+  }
+  pg.qt = qt;
+  if (slab_total && hipMalloc(&pg.slabs, slab_total) != hipSuccess) {
+    (void)hipGetLastError();
+    pg.slabs = nullptr;
+    return fail(LK_ERR_DEVICE, "plan: pair group slabs (%zu B)", slab_total);
+  }
+  for (size_t k = 0; k < nodes.size(); k++) {
+    SkinnyArgs &g = nodes[k];
+    if (g.slices > 1) {
+      g.partial = (float *)((uint8_t *)pg.slabs + slab_off[k]);
+      ReduceNode r{};
+      r.partial = g.partial; r.dst = g.dst; r.d_nb0 = g.d_nb0; r.d_nb1 = g.d_nb1;
+      r.slices = g.slices; r.M = g.M; r.N = g.N; r.N16 = 32;
+      r.threads = (int64_t)g.M * 8;  // one thread per 4 of the 32 padded columns of a row
+      rthreads += (r.threads + 255) / 256 * 256;
+      red.push_back(r);
+    }
+  }
+  pg.nn = (int)nodes.size();
+  pg.nred = (int)red.size();
+  pg.grid = (unsigned)((tasks + 7) / 8 * 8);
+  pg.rgrid = (unsigned)(rthreads / 256);
+  const size_t nb = nodes.size() * sizeof(SkinnyArgs), rb = red.size() * sizeof(ReduceNode);
+  if (hipMalloc((void **)&pg.nodes, nb) != hipSuccess || (rb && hipMalloc((void **)&pg.red, rb) != hipSuccess) ||
+      hipMemcpy(pg.nodes, nodes.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
+      (rb && hipMemcpy(pg.red, red.data(), rb, hipMemcpyHostToDevice) != hipSuccess)) {
+    (void)hipGetLastError();
+    return fail(LK_ERR_DEVICE, "plan: pair group upload");
+  }
+  return LK_OK;
+}
+
+int launch_pair_group(const PairGroupLaunch &pg, hipStream_t st) {
+  note_route("pairgroup<%d,2>:n%dg%u", pg.qt, pg.nn, pg.grid);
+  if (pg.qt == LK_TYPE_Q4_0)
+    hipLaunchKernelGGL((gemm_skinny_pair_group_kernel<LK_TYPE_Q4_0, 2>), dim3(pg.grid), dim3(512),
+                       (SkinnyPairGeom<LK_TYPE_Q4_0, 2>::LDS), st, (const SkinnyArgs *)pg.nodes, pg.nn);
+  else
+    hipLaunchKernelGGL((gemm_skinny_pair_group_kernel<LK_TYPE_Q4_1, 2>), dim3(pg.grid), dim3(512),
+                       (SkinnyPairGeom<LK_TYPE_Q4_1, 2>::LDS), st, (const SkinnyArgs *)pg.nodes, pg.nn);
+  if (pg.nred) hipLaunchKernelGGL(splitk_reduce_group_kernel, dim3(pg.rgrid), dim3(256), 0, st, (const ReduceNode *)pg.red, pg.nred);
   HIP_TRY(hipGetLastError());
   return LK_OK;
 }
@@ -851,9 +948,7 @@ int launch_kpart_t(const SkinnyArgs &s, hipStream_t st) {
   return LK_OK;
 }
 
-int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
-  static const bool no_kpart = getenv_flag("LK_KPART_OFF");  // A/B: the round-3 skinny / pair kernels
-  static const bool kpart_all = getenv_flag("LK_KPART_ALL");  // A/B: every Q4 shape on the kpart kernel
+SkinnyArgs skinny_args(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const Checked &c) {
   SkinnyArgs g{};
   g.a = (const uint8_t *)a->data + a->data_offset;
   g.b = (const uint8_t *)b->data + b->data_offset;
@@ -866,6 +961,13 @@ int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const 
   // A/B three rounds: the shifted rows touch one more line each)
   static const bool shift = getenv_flag("LK_SKP_SHIFT");
   g.shift8 = (shift && a->type == LK_TYPE_Q4_0 && c.a_hi + 8 <= a->buf_bytes) ? 8 : 0;
+  return g;
+}
+
+int launch_skinny(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
+  static const bool no_kpart = getenv_flag("LK_KPART_OFF");  // A/B: the round-3 skinny / pair kernels
+  static const bool kpart_all = getenv_flag("LK_KPART_ALL");  // A/B: every Q4 shape on the kpart kernel
+  SkinnyArgs g = skinny_args(a, b, dst, c);
   // Q4_0 / Q4_1 at N <= 16 with at most two K slices (K <= 4096) on the K-partitioned kernel (round 4:
   // the slices add into dst); otherwise the skinny / pair kernels with the slab reduce launch
   // (measured round 4: N = 8 / 16 16.2 / 16.4 vs 17.5 / 17.7 µs; C3 N = 32 23.3 vs 23.0; the down
@@ -1250,6 +1352,17 @@ int run_single_gemv(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, cons
   if (const int cls = stream_class(a, c))
     return launch_stream(a->type, cls, stream_grid(c.M), d, nullptr, 0, st);
   return launch_gemv_v1(a->type, d, st);
+}
+
+// True when mul_mat_device_checked would run these operands on gemm_skinny_pair_kernel with the slab-sum
+// launch after it (Q4_0 / Q4_1, 17 <= N <= 32, not w32 / kpart): the nodes a plan may group (lk_plan_launch).
+bool pair_routed(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, const Checked &c) {
+  static const bool kpart_all = getenv_flag("LK_KPART_ALL");
+  if (c.empty || c.K == 0 || c.path == Path::kKQuantF32 || c.path == Path::kF32) return false;
+  if (a->type != LK_TYPE_Q4_0 && a->type != LK_TYPE_Q4_1) return false;
+  if (c.N <= 16 || c.N > 32 || kpart_all) return false;
+  if (gemv_eligible(a, b, dst, c) || !gemm_eligible(c) || w32_eligible(a, c) || !skinny_eligible(a, c)) return false;
+  return true;
 }
 
 int mul_mat_device_checked(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Checked &c, hipStream_t st) {
@@ -1822,6 +1935,10 @@ out:
 struct lk_plan {
   struct Group { int32_t qt; int cls; int grid; int spw; StreamWork *work; };
   std::vector<Group> groups;
+  // independent 17 <= N <= 32 Q4 nodes of one type in one gemm_skinny_pair_group_kernel launch plus one
+  // splitk_reduce_group_kernel launch (round 6); slabs owned by the plan, so one plan must not run on two
+  // streams at once (as a chain plan's barrier words)
+  std::vector<PairGroupLaunch> pairs;
   struct Single { lk_tensor a, b, d; Checked c; };
   std::vector<Single> singles;
   unsigned *sync = nullptr;  // chain plans: barrier counters, exit counter, timeout flag
@@ -1834,6 +1951,31 @@ struct lk_plan {
 };
 
 namespace {
+
+// A plan's singles that run on the pair kernel, two or more of one quant type, become one grouped launch
+// (PairGroupLaunch, built before the extern "C" section; LK_PLAN_NO_PAIR_GROUP=1: one launch pair per node,
+// as before; A/B only).
+int group_pair_singles(lk_plan *plan) {
+  static const bool off = getenv_flag("LK_PLAN_NO_PAIR_GROUP");
+  // only nodes small enough that their per-launch fixed cost matters (LK_PLAN_PAIR_GROUP_MB overrides; A/B)
+  static const double max_mb = [] { const char *e = getenv("LK_PLAN_PAIR_GROUP_MB"); return e ? atof(e) : 1e9; }();
+  if (off) return LK_OK;
+  for (int32_t qt : {LK_TYPE_Q4_0, LK_TYPE_Q4_1}) {
+    std::vector<lk_plan::Single> mine, rest;
+    for (auto &sg : plan->singles) {
+      const double mb = (double)sg.c.M * (double)(sg.c.K / 32) * (qt == LK_TYPE_Q4_0 ? 18 : 20) / 1e6;
+      (sg.a.type == qt && mb <= max_mb && pair_routed(&sg.a, &sg.b, &sg.d, sg.c) ? mine : rest).push_back(sg);
+    }
+    if (mine.size() < 2) continue;
+    std::vector<PairNodeOps> ops;
+    for (auto &sg : mine) ops.push_back({&sg.a, &sg.b, &sg.d, &sg.c});
+    plan->pairs.emplace_back();
+    const int rc = build_pair_group(qt, ops, plan->pairs.back());  // freed by lk_plan_destroy on failure too
+    if (rc) return rc;
+    plan->singles.swap(rest);
+  }
+  return LK_OK;
+}
 
 // Workgroup g gets global rows [bound[g], bound[g+1]) of the concatenation of descs,
 // balanced by weight bytes, cut at node boundaries into segments.
@@ -2004,6 +2146,7 @@ int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst,
     }
     else plan->singles.push_back({a[i], b[i], dst[i], c});
   }
+  if ((rc = group_pair_singles(plan))) { lk_plan_destroy(plan); return rc; }
   for (auto &kv : by_type) {
     const int32_t qt = kv.first;
     const int cls = type_cls[qt];
@@ -2189,6 +2332,10 @@ int lk_plan_launch(lk_plan *plan, void *stream) {
     int rc = launch_stream(g.qt, g.cls, g.grid, pf, g.work, g.spw, st, plan->peer);
     if (rc) return rc;
   }
+  for (auto &pg : plan->pairs) {
+    int rc = launch_pair_group(pg, st);
+    if (rc) return rc;
+  }
   for (auto &s : plan->singles) {
     int rc = mul_mat_device_checked(&s.a, &s.b, &s.d, s.c, st);
     if (rc) return rc;
@@ -2213,12 +2360,13 @@ extern "C" int lk_plan_prefetch_next(lk_plan *plan, const lk_plan *next) {
 #endif
 
 int lk_plan_num_launches(const lk_plan *plan) {
-  return plan ? (int)(plan->groups.size() + plan->singles.size()) : 0;
+  return plan ? (int)(plan->groups.size() + plan->pairs.size() + plan->singles.size()) : 0;
 }
 
 void lk_plan_destroy(lk_plan *plan) {
   if (!plan) return;
   for (auto &g : plan->groups) (void)hipFree(g.work);
+  for (auto &pg : plan->pairs) free_pair_group(pg);
   if (plan->sync) (void)hipFree(plan->sync);
   delete plan;
 }

@@ -2125,7 +2125,7 @@ __device__ __forceinline__ void lds_st(int *p, int v) {
 }
 
 template <int QT, int NT>
-__global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
+__device__ __forceinline__ void skinny_pair_body(const SkinnyArgs &g, int task) {
   using G = SkinnyPairGeom<QT, NT>;
   constexpr int BB = G::BB, D = G::D, L = G::L, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2137,9 +2137,6 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int p = wave & 3, h = wave >> 2;
   uint8_t *ring = smem + G::XB + G::TB + G::EB + G::FB + wave * D * G::SLOT;
-  // XCD-aware task order, as gemm_skinny_kernel
-  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
-  if (task >= g.tasks) return;  // grid padding (before any barrier: the whole workgroup leaves)
   [[maybe_unused]] const uint64_t t_entry = LK_KP_T();
   if (threadIdx.x < 16) flags[threadIdx.x] = 0;  // published by the prologue's barrier
   const int slice = task % g.slices, range = task / g.slices;
@@ -2356,6 +2353,46 @@ __global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
   LK_KP_SET(0, t_entry); LK_KP_SET(2, t_loop); LK_KP_SET(3, t_end); LK_KP_SET(4, LK_KP_T());
   LK_KP_SET(8, (uint64_t)nunits); LK_KP_SET(1, t_split); LK_KP_SET(5, t_issued); LK_KP_SET(6, t_bar);
 }
+
+template <int QT, int NT>
+__global__ __launch_bounds__(512) void gemm_skinny_pair_kernel(SkinnyArgs g) {
+  // XCD-aware task order, as gemm_skinny_kernel (a single node: the grouped kernel's interleaved order
+  // measured the same on C3, 20.2-20.9 vs 20.2-21.0 us, A/B three rounds)
+  const int task = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+  if (task >= g.tasks) return;  // grid padding (before any barrier: the whole workgroup leaves)
+  skinny_pair_body<QT, NT>(g, task);
+}
+
+// Several independent nodes of one plan in ONE launch (round 6, lk_plan_launch's grouped singles): node
+// k's tasks follow node k − 1's in the grid, each with the SkinnyArgs the single-node launch would use
+// (same ranges, slices, slabs: the same bits). The per-node launch gaps and tails of a plan's 2 <= N <= 32
+// nodes overlap instead of adding up.
+template <int QT, int NT>
+__global__ __launch_bounds__(512) void gemm_skinny_pair_group_kernel(const SkinnyArgs *__restrict__ nodes, int nnodes) {
+  // task = workgroup index (no XCD-contiguous runs): dispatch deals consecutive workgroups to the 8 XCDs
+  // in turn, so every node's tasks spread over all XCDs and the dispatcher balances nodes of different
+  // per-task cost (XCD-contiguous runs gave some XCDs only the heavy nodes: the layer set 4 % slower than
+  // separate launches); a node's slice s (= task % 8 at 8 slices) then stays on one XCD, whose L2 serves
+  // its activation slice to all of that XCD's ranges
+  int task = (int)blockIdx.x;
+  for (int k = 0; k < nnodes; k++) {
+    const int tk = nodes[k].tasks;
+    if (task < tk) {
+      skinny_pair_body<QT, NT>(nodes[k], task);
+      return;
+    }
+    task -= tk;
+  }
+}
+
+// splitk_reduce_kernel over a plan's grouped nodes: node k's threads follow node k − 1's.
+struct ReduceNode {
+  const float *partial;
+  uint8_t *dst;
+  int64_t d_nb0, d_nb1;
+  int32_t slices, M, N, N16;
+  int64_t threads;  // M·N16/4
+};
 
 // ---- wide batched GEMM (N > 32, e.g. C5's prefill N = 512): 256-row tiles, 8 waves ----------
 //
@@ -2739,9 +2776,29 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(WideArgs g) {
 
 // dst(n, m) = Σ_s P[s][m][n], slices in order (deterministic); one thread per 4 columns.
 #ifndef LK_W32_KERNELS  // (lk_w32.hip includes this header for its helpers only)
+__device__ __forceinline__ void splitk_reduce_body(const float *__restrict__ P, int slices, int M, int N, int N16,
+                                                   uint8_t *__restrict__ dst, int64_t d_nb0, int64_t d_nb1, int64_t idx);
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restrict__ P, int slices, int M, int N, int N16,
                                                             uint8_t *__restrict__ dst, int64_t d_nb0, int64_t d_nb1) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  splitk_reduce_body(P, slices, M, N, N16, dst, d_nb0, d_nb1, (int64_t)blockIdx.x * 256 + threadIdx.x);
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_group_kernel(const ReduceNode *__restrict__ nodes, int nnodes) {
+  int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int k = 0; k < nnodes; k++) {
+    const int64_t blocks = (nodes[k].threads + 255) / 256 * 256;  // each node starts on a block boundary
+    if (idx < blocks) {
+      const ReduceNode &r = nodes[k];
+      splitk_reduce_body(r.partial, r.slices, r.M, r.N, r.N16, r.dst, r.d_nb0, r.d_nb1, idx);
+      return;
+    }
+    idx -= blocks;
+  }
+}
+
+__device__ __forceinline__ void splitk_reduce_body(const float *__restrict__ P, int slices, int M, int N, int N16,
+                                                   uint8_t *__restrict__ dst, int64_t d_nb0, int64_t d_nb1, int64_t idx) {
   const int c4 = N16 / 4;
   if (idx >= (int64_t)M * c4) return;
   const int64_t m = idx / c4;

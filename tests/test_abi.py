@@ -56,6 +56,7 @@ PRODUCT_KERNELS = {
     "kquant_gemv_kernel", "kquant_mul_mat_kernel", "mul_mat_generic_kernel", "dequantize_coop_kernel",
     "quantize_coop_kernel", "dequantize_kernel", "quantize_kernel", "dot_direct_kernel",
     "repack_q4_kernel", "gemv_stream_peer_kernel", "gemm_w32_kernel", "xsplit32_kernel",
+    "gemm_skinny_pair_group_kernel", "splitk_reduce_group_kernel",
 }
 
 

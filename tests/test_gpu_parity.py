@@ -271,6 +271,53 @@ def test_plan_equals_single_launches(gpu, oracle):
         assert ok, msg
 
 
+def test_plan_groups_pair_nodes(gpu, oracle):
+    """Round 6: a plan's independent 17 <= N <= 32 Q4_0 / Q4_1 nodes run as ONE grouped pair-kernel launch
+    per type plus one grouped slab-sum launch (lk_plan_launch) — the same bits as one launch each, on the
+    oracle; one slice, several slices, ragged rows and columns, K = 11008; a second plan launch reuses the
+    plan's slabs bit-equal."""
+    import torch
+    import ggml_hip as G
+    O = oracle
+    ga = G.GGMLGraphAllocator(defaultBufferSize=1 << 26)
+    specs = [(2, 256, 4096, 32), (2, 200, 1024, 24), (2, 64, 512, 32), (2, 1000, 11008, 17),
+             (3, 300, 2048, 32), (3, 48, 4096, 20), (2, 96, 256, 8)]  # the last (N = 8) stays a single launch
+    nodes, refs, noises = [], [], []
+    for i, (qt, M, K, N) in enumerate(specs):
+        q, x = make_inputs(O, qt, M, K, N, seed=40 + i)
+        a = ga.allocateTensor(G.GGMLType(qt), [K, M]); ga.setTensorBytes(a, q)
+        b = ga.allocateTensor(G.GGMLType.F32, [N, K]); ga.setTensorBytes(b, np.ascontiguousarray(x, np.float32).view(np.uint8).reshape(-1))
+        d = ga.allocateTensor(G.GGMLType.F32, [N, M])
+        nodes.append((a, b, d))
+        refs.append(O.mat_mul_q(qt, q, M, K, x))
+        noises.append(noise_for(O, qt, q, M, K, x))
+    plan = G.MulMatPlan(ga, nodes)
+    assert plan.numLaunches == 3  # the Q4_0 group, the Q4_1 group, the N = 8 node
+    G.debugRoute()
+    plan.launch()
+    torch.cuda.synchronize()
+    route = G.debugRoute()
+    assert "pairgroup<2,2>:n4" in route and "pairgroup<3,2>:n2" in route, route
+
+    def outs():
+        return [ga.tensorBytes(d).cpu().numpy().view(np.float32).copy() for (_, _, d) in nodes]
+
+    grouped = outs()
+    plan.launch()
+    torch.cuda.synchronize()
+    again = outs()
+    for (a, b, d) in nodes:
+        G.computeMatMul(ga, ga.context, a, b, d)
+    torch.cuda.synchronize()
+    single = outs()
+    for (qt, M, K, N), gr, ag, sg, ref, nz in zip(specs, grouped, again, single, refs, noises):
+        assert np.array_equal(gr.view(np.uint32), sg.view(np.uint32)), (qt, M, K, N)
+        assert np.array_equal(ag.view(np.uint32), sg.view(np.uint32)), (qt, M, K, N)
+        ok, msg = parity_ok(sg.reshape(M, N), ref, noise=nz)
+        assert ok, ((qt, M, K, N), msg)
+    plan.close()
+
+
 def test_backend_graph_compute(gpu, oracle):
     import ggml_hip as G
     O = oracle
