@@ -692,7 +692,11 @@ size_t pair_geometry(SkinnyArgs &g) {
   const int nblk = g.K / 32;
   const int slices = (nblk + SG::SB - 1) / SG::SB;
   const int ntile = (g.M + 15) / 16;
-  int ranges = std::max(1, std::min(ntile, cu_count() / slices));
+  // at least one tile per stream (4 wave pairs per workgroup): small matrices (a 1/8-row shard) otherwise
+  // got one tile per workgroup, three of its four streams idle behind the full activation prologue.
+  // Ranges only partition tiles among workgroups, so the bits do not depend on it.
+  static const int min_tpr = [] { const char *e = getenv("LK_SKP_MIN_TPR"); return e ? std::max(1, atoi(e)) : 4; }();
+  int ranges = std::max(1, std::min({ntile, cu_count() / slices, (ntile + min_tpr - 1) / min_tpr}));
   g.tiles_per_range = (ntile + ranges - 1) / ranges;
   ranges = (ntile + g.tiles_per_range - 1) / g.tiles_per_range;
   g.slices = slices;
