@@ -72,7 +72,7 @@ def _oracle_check(ga, oracle, nodes, x, got):
     return out
 
 
-@pytest.mark.parametrize("N", [1, 4])
+@pytest.mark.parametrize("N", [1, 4, 32])  # 32: the level's Q4_0 nodes as one grouped pair launch (round 6)
 def test_layer_graph_equals_sequential(gpu, oracle, N):
     """The resident graph and the node-by-node path must agree bit for bit, and BOTH must meet the
     parity bar against the oracle: a difference says which side is wrong, and the failure message
@@ -96,6 +96,8 @@ def test_layer_graph_equals_sequential(gpu, oracle, N):
     got = [bytes(ga.tensorBytes(d)) for _, _, d in nodes]
     graph_ok = _oracle_check(ga, oracle, nodes, x, got)
     ctr = G.syncCountersSum()
+    if N == 32:  # the first level's three Q4_0 nodes (q, g, u) run as one grouped launch
+        assert "pairgroup<2,2>:n3" in groute, groute
     diag = "\n".join(f"  {n}: node-by-node {seq_ok[n]} route [{r}] | graph {graph_ok[n]}"
                       for n, r in zip(NAMES, routes)) + f"\n  graph route [{groute}]\n  counters {ctr}"
     if os.environ.get("LK_DIAG_DUMP") and not all(ok for ok, _ in seq_ok.values()):  # lab diagnostic
