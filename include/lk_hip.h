@@ -174,10 +174,13 @@ int lk_mul_mat_sharded_at(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst
 
 typedef struct lk_plan lk_plan;
 /* Validate n independent nodes (device buffers) and upload their descriptors once.
- * Nodes with the same quant type are executed by one grouped launch each. */
+ * Batch-1 streaming nodes with the same quant type run as one grouped launch each; since round 6
+ * so do Q4_0 / Q4_1 nodes at 17 <= N <= 32 (one pair-kernel launch + one slab-sum launch per type,
+ * the same bits as single launches; split-K slabs owned by the plan). */
 int lk_plan_create(const lk_tensor *a, const lk_tensor *b, const lk_tensor *dst, int n,
                    lk_plan **out);
-/* Enqueue every node of the plan on `stream`. */
+/* Enqueue every node of the plan on `stream`. A plan's launches are stream-ordered: one plan must not
+ * run on two streams at once (its slabs and, for chain plans, its barrier words are its own). */
 int lk_plan_launch(lk_plan *plan, void *stream);
 /* Number of kernel launches one lk_plan_launch issues. */
 int lk_plan_num_launches(const lk_plan *plan);
