@@ -37,6 +37,9 @@
 #ifndef LK_W32_PRIO
 #define LK_W32_PRIO 1  // issue priority 1 for the second-dispatched row half (waves 4-7): 52.2-52.5 us vs 54.0 at C5 (lab: 0)
 #endif
+#ifndef LK_W32_ILV
+#define LK_W32_ILV 1  // the chains' MFMAs interleaved step by step (C5 50.6-51.3 vs 51.5-51.9 us; lab: 0 = chain by chain)
+#endif
 #ifndef LK_W32_PP
 #define LK_W32_PP 0  // lab: 1 = the two row halves in ping-pong (w32_main_pp): C5 53.8-54.0 vs 52.3-52.6 us, not kept
 #endif
@@ -231,6 +234,9 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
     for (int c = c0; c < c1; c++) {
       const int q = wave * CW + c;
       const uint8_t *base = kind[c] == 0 ? bw : kind[c] == 1 ? bx : bt;
+#ifdef LK_LAB_W32_NO_XDMA  // skeleton (wrong results): the fragments' DMA instructions read one 16-B line
+      if (kind[c] == 1) { dma16m(bx, 0u, slot + W::PAD_OFF); continue; }
+#endif
       dma16m(base, vofs[c], kind[c] == 3 ? slot + W::PAD_OFF : slot + q * 1024);
     }
   };
@@ -296,6 +302,13 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
 #else
         const LK_LDS uint8_t *f = px + (j * W::SB * 4 + s2 * 2) * 1024;
 #endif
+#ifdef LK_LAB_W32_NO_XREAD  // skeleton (wrong results): fragments from registers, no LDS reads
+        const uint32_t z = (uint32_t)(lane * 3 + j * 5 + s2 * 7 + st);
+        xh[s2] = __builtin_bit_cast(bf16x8, u32x4{z, z ^ 1u, z ^ 2u, z ^ 3u});
+        xl[s2] = __builtin_bit_cast(bf16x8, u32x4{z ^ 4u, z ^ 5u, z ^ 6u, z ^ 7u});
+        (void)f;
+        continue;
+#endif
         xh[s2] = __builtin_bit_cast(bf16x8, *(const LK_LDS u32x4 *)f);
         xl[s2] = __builtin_bit_cast(bf16x8, *(const LK_LDS u32x4 *)(f + 1024));
       }
@@ -348,6 +361,39 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
       }
 #endif
     };
+#if LK_W32_ILV
+    // the MT·NT chains' MFMAs interleaved step by step (each chain's own order unchanged: the same bits),
+    // so no MFMA waits on the one before it; every column tile's fragments and T live at once
+    bf16x8 xhj[NT][2], xlj[NT][2];
+    f32x16 Tj[NT];
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      load_x(j);
+      xhj[j][0] = xh[0]; xhj[j][1] = xh[1]; xlj[j][0] = xl[0]; xlj[j][1] = xl[1];
+      Tj[j] = T;
+    }
+    f32x16 pc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+      for (int j = 0; j < NT; j++) pc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xlj[j][0], w0[i], Tj[j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+      for (int j = 0; j < NT; j++) pc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xhj[j][0], w0[i], pc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+      for (int j = 0; j < NT; j++) pc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xlj[j][1], w1[i], pc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+      for (int j = 0; j < NT; j++) pc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xhj[j][1], w1[i], pc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MT; i++)
+#pragma unroll
+      for (int j = 0; j < NT; j++) scale(i, j, pc[i][j], Tj[j]);
+#else
     f32x16 pa, ta;
     int pi = 0, pj = 0;
 #pragma unroll
@@ -367,6 +413,7 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
       }
     }
     scale(MT - 1, NT - 1, pa, ta);
+#endif
 #if LK_W32_SCHED
     // one MFMA, then its share of the VALU (decode + scale FMAs), so the VALU issues in the MFMAs' shadow
 #pragma unroll
