@@ -323,7 +323,7 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
       }
 #endif
     };
-    auto chain = [&](int i) __attribute__((always_inline)) -> f32x16 {
+    [[maybe_unused]] auto chain = [&](int i) __attribute__((always_inline)) -> f32x16 {
 #ifdef LK_LAB_W32_NO_MFMA  // skeleton (wrong results): operands consumed by one VALU op, no MFMA
       f32x16 q = T;
       q[0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, xl[0]).x ^ __builtin_bit_cast(u32x4, xh[0]).y ^
