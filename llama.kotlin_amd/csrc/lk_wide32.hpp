@@ -1,5 +1,6 @@
-// lk_wide32.hpp — Q4_0 / Q4_1 x F32 at N > 16 on v_mfma_f32_32x32x16_bf16, one wave per SIMD
-// (round 6): config C5 (4096 x 4096, batch 512) and the skinny config C3 (11008 x 4096, batch 32).
+// lk_wide32.hpp — Q4_0 / Q4_1 x F32 at N > 32 on v_mfma_f32_32x32x16_bf16 (round 6): config C5 (4096 x
+// 4096, batch 512) and every N > 32 shape that meets w32_eligible (csrc/lk_hip.hip); N <= 32 stays on the
+// pair / kpart kernels (this kernel's <3,1,1> shape measured slower on C3).
 //
 // Arithmetic (the reference's, K/core/GGMLComputeOps.kt:70-145, within the F32 bar): per 32-weight block
 // b of row m and activation column n, with the codes as exact bf16 128 + q and x = hi + lo in bf16 pairs
@@ -8,26 +9,24 @@
 // acc += d·p (Q4_1: + m·Σx = (−m/128)·T) in f32 with the block's f16 scale d, so an Inf / NaN scale gives
 // what d·p gives (tests/test_gpu_parity.py::test_w32_route_and_nonfinite_scales).
 //
-// Why this shape: gemm_wide_kernel (8 waves, 16x16x32, 256 x 64 tiles, K split in
-// two) was LDS-read bound — per 16-cycle MFMA ~480 B of LDS reads (x fragments re-read by every row tile
-// of a wave, 4-way-conflicting ds_read_b32 weight reads, T as 1 KB per block and column tile) — and its
-// two K slices wrote 16 MB of slabs at C5. Here:
-//   * a workgroup is BM = 32·MT rows x BN = 32·NT columns, 4 waves (one per SIMD: a wave owns the SIMD's
-//     512 registers and hides its ~5 VALU per MFMA behind the matrix pipe, MI355X_MICROARCH.md);
-//   * the 4 waves split each 4-block stage's K: wave g takes block g over the FULL tile (MT x NT chains
-//     of 32 x 32), so every fragment and weight byte in LDS is read by exactly one wave and a decoded
-//     weight fragment feeds NT column tiles;
-//   * 32x32x16: an MFMA holds the SIMD's issue for 8 of its 32 cycles (16x16x32: 8 of 16), leaving room
-//     for the decode (7 VALU per 8 codes) and the 16 scale FMAs per chain and block;
+// Shape: gemm_wide_kernel (16x16x32, 256 x 64 tiles, K split in two) was LDS-read bound and
+// its two K slices wrote 16 MB of slabs at C5. Here:
+//   * a workgroup is MH row halves of 32·MT rows x BN = 32·NT columns; 4·MH waves, wave w takes K group
+//     w % 4 of row half w / 4 — the product <2,2,2>: 128 x 64 tiles, 8 waves, two per SIMD (one of each
+//     half), issue priority 1 for the second-dispatched half (LK_W32_PRIO);
+//   * the 4 K groups split each 4-block stage's K: group g takes block g over its half's MT x NT chains
+//     of 32 x 32, so a decoded weight fragment feeds NT column tiles; the chains' MFMAs are interleaved
+//     step by step (LK_W32_ILV), each chain's order unchanged;
 //   * C layout: one weight row per lane (col = lane & 31), so the block scale is a per-lane scalar; T is
 //     16 values per lane, broadcast ds_read_b128 from a 1-KB stage slot;
-//   * weights: each row's 4-block window (72 / 80 B in 5 16-B pieces) by LDS-DMA; a lane reads the two
-//     pieces holding its block (conflict-free ds_read_b128 at the 5-piece pitch) and aligns its 8 code
-//     bytes in registers;
+//   * one LDS-DMA ring of D = 3 stages (the tile's 80-B weight windows, the 64 columns' fragments, T:
+//     44 KB), one workgroup barrier per stage, every wave issuing its share of the next stage's DMA;
+//     a lane reads the two pieces holding its block and aligns its 8 code bytes in registers;
 //   * the 4 K groups are summed through LDS in group order (deterministic); with `slices` > 1 (K split
-//     over workgroups, C3's shapes) each slice stores its partial write-through and the last to arrive
-//     at the tile's counter sums the slabs in slice order (no waits);
-//   * blockIdx -> task XCD-aware: each XCD takes a contiguous run of tasks, column tile major.
+//     over workgroups when the tiles leave CUs idle) each slice stores its partial write-through and the
+//     last to arrive at the tile's counter sums the slabs in slice order (no waits);
+//   * blockIdx -> task XCD-aware: each XCD takes a contiguous run of tasks, grouped by `bc` column tiles
+//     so a run covers a block of row x column tiles (W32Args::bc).
 #ifndef LK_W32_PK
 #define LK_W32_PK 1  // packed scale FMAs (lab: 0 = scalar)
 #endif
