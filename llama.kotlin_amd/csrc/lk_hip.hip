@@ -1128,7 +1128,7 @@ int launch_w32(const lk_tensor *a, const lk_tensor *b, lk_tensor *dst, const Che
   g.dst = (uint8_t *)dst->data + dst->data_offset;
   g.d_nb0 = dst->nb[0]; g.d_nb1 = dst->nb[1];
   g.M = (int32_t)c.M; g.N = (int32_t)c.N; g.K = (int32_t)c.K;
-  w32_launch_xsplit(xa, (unsigned)((ntx * nblk + 3) / 4), st);
+  w32_launch_xsplit(xa, (unsigned)(ntx * nblk), st);
   const bool q41 = a->type == LK_TYPE_Q4_1;
   static const int cfg = [] { const char *e = getenv("LK_W32_CFG"); return e ? atoi(e) : 0; }();  // A/B only
   if (c.N > 32) {

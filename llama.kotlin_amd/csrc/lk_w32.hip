@@ -13,7 +13,8 @@
 
 namespace lk {
 
-void w32_launch_xsplit(const XSplit32Args &xa, unsigned grid, hipStream_t st) {
+void w32_launch_xsplit(const XSplit32Args &xa, unsigned items, hipStream_t st) {
+  const unsigned grid = (items + 4 * LK_XS32_IPW - 1) / (4 * LK_XS32_IPW);  // 4 waves per workgroup
   hipLaunchKernelGGL(xsplit32_kernel, dim3(grid), dim3(256), 0, st, xa);
 }
 

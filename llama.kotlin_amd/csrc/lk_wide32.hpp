@@ -99,47 +99,61 @@ struct XSplit32Args {
 // x(n, 32kb + 8(2h + s) + ord[j]) (ord = 0,4,1,5,2,6,3,7: q4_codes_128's element order of code dword
 // 2h + s) split into bf16 hi (truncated) and lo (x − hi rounded to nearest even), as fragment
 // ((t·nblk + kb)·2 + s)·2 + {0: hi, 1: lo}; and T = mult·Σ (hi + lo) over the block's 32 k.
+#ifndef LK_XS32_IPW
+#define LK_XS32_IPW 2  // (column tile, block) items per wave, both items' loads in flight together: C5 -0.3-0.5 us (1: +0.4, 4: +1.3, A/B)
+#endif
 __global__ __launch_bounds__(256) void xsplit32_kernel(XSplit32Args g) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
-  const int64_t nblk = g.K / 32, ntx = (g.N + 31) / 32, item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (item >= ntx * nblk) return;
-  const int64_t t = item / nblk, kb = item % nblk;
-  const int64_t n = 32 * t + (lane & 31);
-  float v[2][8];
+  const int64_t nblk = g.K / 32, ntx = (g.N + 31) / 32, item0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LK_XS32_IPW;
+  if (item0 >= ntx * nblk) return;
+  float v[LK_XS32_IPW][2][8];
 #pragma unroll
-  for (int s = 0; s < 2; s++)
+  for (int it = 0; it < LK_XS32_IPW; it++) {
+    const int64_t item = min(item0 + it, ntx * nblk - 1);
+    const int64_t t = item / nblk, kb = item % nblk;
+    const int64_t n = 32 * t + (lane & 31);
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const int64_t k = 32 * kb + 8 * (2 * h + s) + ((j >> 1) + 4 * (j & 1));
-      v[s][j] = n < g.N ? *(const float *)(g.b + n * g.b_nb0 + k * g.b_nb1) : 0.f;
-    }
-  float sum = 0.f;
+    for (int s = 0; s < 2; s++)
 #pragma unroll
-  for (int s = 0; s < 2; s++) {
-    uint32_t hi[4], lo[4];
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      uint32_t hb[2], lb[2];
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const uint32_t bx = __builtin_bit_cast(uint32_t, v[s][j + q]);
-        const float hf = __builtin_bit_cast(float, bx & 0xFFFF0000u);
-        const float r = v[s][j + q] - hf;  // exact
-        uint32_t br = __builtin_bit_cast(uint32_t, r);
-        br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even (r is finite, |r| < 2^-7·|x|)
-        hb[q] = bx;
-        lb[q] = br;
-        sum += hf + __builtin_bit_cast(float, br & 0xFFFF0000u);
+      for (int j = 0; j < 8; j++) {
+        const int64_t k = 32 * kb + 8 * (2 * h + s) + ((j >> 1) + 4 * (j & 1));
+        v[it][s][j] = n < g.N ? *(const float *)(g.b + n * g.b_nb0 + k * g.b_nb1) : 0.f;
       }
-      hi[j / 2] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
-      lo[j / 2] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
-    }
-    u32x4 *f = g.frag + ((item * 2 + s) * 2) * 64 + lane;
-    f[0] = u32x4{hi[0], hi[1], hi[2], hi[3]};
-    f[64] = u32x4{lo[0], lo[1], lo[2], lo[3]};
   }
-  sum += __shfl_xor(sum, 32, kWave);
-  if (h == 0) g.tsum[kb * (ntx * 32) + n] = g.mult * sum;
+#pragma unroll
+  for (int it = 0; it < LK_XS32_IPW; it++) {
+    const int64_t item = item0 + it;
+    if (item >= ntx * nblk) break;
+    const int64_t t = item / nblk, kb = item % nblk;
+    const int64_t n = 32 * t + (lane & 31);
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      uint32_t hi[4], lo[4];
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        uint32_t hb[2], lb[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          const uint32_t bx = __builtin_bit_cast(uint32_t, v[it][s][j + q]);
+          const float hf = __builtin_bit_cast(float, bx & 0xFFFF0000u);
+          const float r = v[it][s][j + q] - hf;  // exact
+          uint32_t br = __builtin_bit_cast(uint32_t, r);
+          br += 0x7FFFu + ((br >> 16) & 1u);  // round to nearest even (r is finite, |r| < 2^-7·|x|)
+          hb[q] = bx;
+          lb[q] = br;
+          sum += hf + __builtin_bit_cast(float, br & 0xFFFF0000u);
+        }
+        hi[j / 2] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+        lo[j / 2] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+      }
+      u32x4 *f = g.frag + ((item * 2 + s) * 2) * 64 + lane;
+      f[0] = u32x4{hi[0], hi[1], hi[2], hi[3]};
+      f[64] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+    }
+    sum += __shfl_xor(sum, 32, kWave);
+    if (h == 0) g.tsum[kb * (ntx * 32) + n] = g.mult * sum;
+  }
 }
 
 // Block G of a stage window, from its two 16-B pieces G, G + 1 (window bytes [16G, 16G + 32); the block
@@ -764,7 +778,7 @@ __global__ __launch_bounds__(256 * MH, MH) void gemm_w32_kernel(W32Args g) {
 #endif  // LK_W32_KERNELS
 
 // Launchers (lk_w32.hip): enqueue on `st`; hipGetLastError is the caller's.
-void w32_launch_xsplit(const XSplit32Args &xa, unsigned grid, hipStream_t st);
+void w32_launch_xsplit(const XSplit32Args &xa, unsigned items, hipStream_t st);  // items = column tiles x blocks
 void w32_launch(int qt, int mt, int nt, int mh, const W32Args &g, unsigned grid, size_t lds, hipStream_t st);
 
 }  // namespace lk
