@@ -42,6 +42,10 @@
 #ifndef LK_W32_PP
 #define LK_W32_PP 0  // lab: 1 = the two row halves in ping-pong (w32_main_pp): C5 53.8-54.0 vs 52.3-52.6 us, not kept
 #endif
+#ifndef LK_W32_ILDMA
+#define LK_W32_ILDMA 2  // the stage's refill DMAs one by one between its MFMAs, not as a burst after the barrier:
+                        // 2 = DMA c after MFMA c (C5 51.8-52.6 vs 52.7-52.9 us), 1 = spread evenly (~ -0.3 us), 0 = burst
+#endif
 #ifndef LK_W32_SCHED
 #define LK_W32_SCHED 0  // lab: VALU instructions per MFMA enforced by sched_group_barrier (0: the compiler's order)
 #endif
@@ -274,6 +278,8 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
     const uint64_t ti0 = LK_W32_T();
 #endif
 #if defined(LK_LAB_W32_NO_REFILL)  // skeleton (wrong results): the prologue's stages only
+#elif LK_W32_ILV && LK_W32_ILDMA
+    // (issued between the MFMAs below)
 #elif LK_W32_SPREAD
     issue(st + D - 1, (st + D - 1) % D, 0, (CW + 1) / 2);  // refill the slot stage st − 1 used: half now,
 #else
@@ -386,6 +392,28 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
       Tj[j] = T;
     }
     f32x16 pc[MT][NT];
+#if LK_W32_ILDMA && !defined(LK_LAB_W32_NO_REFILL)
+    // the MFMAs in the same order, with refill DMA c issued after MFMA c (LK_W32_ILDMA 2; 1: after MFMA
+    // ((c + 1)·NM)/(CW + 1) − 1): a piece issued in a burst right after the barrier costs its wave ~100
+    // issue cycles, between MFMAs a fraction of that (MI355X_MICROARCH.md, LDS-DMA piece issue cost);
+    // the scheduling barriers keep the compiler from regrouping them. (Between the chains' scale FMAs
+    // instead: C5 53.3-53.9 us, slower.)
+    constexpr int NM = 4 * MT * NT;
+#pragma unroll
+    for (int k = 0; k < NM; k++) {
+      const int s4 = k / (MT * NT), i = (k / NT) % MT, j = k % NT;
+      const bf16x8 xa = s4 == 0 ? xlj[j][0] : s4 == 1 ? xhj[j][0] : s4 == 2 ? xlj[j][1] : xhj[j][1];
+      const bf16x8 wa = s4 < 2 ? w0[i] : w1[i];
+      pc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, wa, s4 == 0 ? Tj[j] : pc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int c = 0; c < CW; c++)
+        if (LK_W32_ILDMA == 1 ? ((c + 1) * NM) / (CW + 1) - 1 == k : LK_W32_ILDMA == 2 ? min(c, NM - 1) == k : false) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue(st + D - 1, (st + D - 1) % D, c, c + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#else
 #pragma unroll
     for (int i = 0; i < MT; i++)
 #pragma unroll
@@ -402,10 +430,13 @@ __device__ __forceinline__ void w32_main(const W32Args &g, uint8_t *smem, int tm
     for (int i = 0; i < MT; i++)
 #pragma unroll
       for (int j = 0; j < NT; j++) pc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xhj[j][1], w1[i], pc[i][j], 0, 0, 0);
+#endif
 #pragma unroll
     for (int i = 0; i < MT; i++)
 #pragma unroll
-      for (int j = 0; j < NT; j++) scale(i, j, pc[i][j], Tj[j]);
+      for (int j = 0; j < NT; j++) {
+        scale(i, j, pc[i][j], Tj[j]);
+      }
 #else
     f32x16 pa, ta;
     int pi = 0, pj = 0;
