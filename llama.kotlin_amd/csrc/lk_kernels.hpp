@@ -340,6 +340,9 @@ template <int QT> constexpr int stream_pb() {
   else if constexpr (QT == LK_TYPE_Q2_K) return LK_Q2_K_BLOCK_BYTES / 4;
   else return 2 * QTraits<QT>::BB;
 }
+#ifndef LK_STREAM_D
+#define LK_STREAM_D 3  // stream-kernel ring depth cap (lab: deeper rings)
+#endif
 template <int QT, int CPL> struct StreamGeom {
   // bytes per 64 items (a lane's share of a unit): a block pair, or a quarter Q4_K block
   static constexpr int PB = stream_pb<QT>();
@@ -351,7 +354,7 @@ template <int QT, int CPL> struct StreamGeom {
   static constexpr bool KQ = QT == LK_TYPE_Q4_K || QT == LK_TYPE_Q2_K;
   static constexpr int AUX = KQ ? 256 : 0;                // K-quants: the i/63 (Q4_K) or i/15 (Q2_K) table
   static constexpr int DFIT = (kLdsBytes - IMG - AUX) / (kStreamWaves * SLOT);
-  static constexpr int D = DFIT < 3 ? DFIT : 3;           // ring depth (units in flight per wave)
+  static constexpr int D = DFIT < LK_STREAM_D ? DFIT : LK_STREAM_D;  // ring depth (units in flight per wave)
   static constexpr int TOFF = IMG + kStreamWaves * D * SLOT;
   static constexpr int LDS = TOFF + AUX;
   static constexpr int VMCNT = (D - 1) * L;               // DMA ops allowed in flight past the unit in use
